@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident CRC-32 (Ethernet FCS) throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s of CRC-32 over device-resident 1500-byte frames,
+with the fraction of the HBM3E read roofline.  One "step" = one
+lnx_crc32_batch call over the rank's whole frame batch (inputs already in HBM).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+N=1 runs BASELINE configs[1] (1 M x 1500 B).  For N>1 (launched by
+torch.distributed.run, one rank per GPU) every rank owns its own contiguous
+slice of configs[4] (128 M x 1500 B over 8 GPUs = 16 M frames per GPU); frames
+are partitioned by index with no data-path collective (weak scaling).  The
+barrier / MAX-over-ranks timing uses torch.distributed (RCCL) only for the
+clock, never for data.
+
+Rank 0 prints ONE JSON line.  Extra fields: "roofline" (dominant kernel,
+HIP-event timed on its launch stream), "cpu_baseline" (the C oracle on the
+box's host cores, bounded sample, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+FRAME_BYTES = 1500
+
+
+def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous frame-index slice [lo, hi) of rank `rank`."""
+    per = (n_total + world - 1) // world
+    lo = min(rank * per, n_total)
+    hi = min(lo + per, n_total)
+    return lo, hi
+
+
+def workload_spec(name: str, world: int):
+    """(frames on this rank, frame length or None for zipf, description)."""
+    if name == "auto":
+        name = "mtu1500" if world == 1 else "mtu1500_x8"
+    if name == "mtu1500":
+        return name, 1 << 20, 1500, "configs[1]: 1M x 1500B device-resident, 1 GPU"
+    if name == "mtu1500_x8":
+        return name, (1 << 27) // 8, 1500, "configs[4]: 128M x 1500B over 8 GPUs (16M per GPU), per-GPU partition"
+    if name == "jumbo9000":
+        return name, 1 << 20, 9000, "configs[2]: 1M x 9000B device-resident, 1 GPU"
+    if name == "zipf64_1500":
+        return name, 1 << 24, None, "configs[3]: 16M mixed 64-1500B (Zipf s=1), 1 GPU"
+    raise SystemExit(f"unknown workload {name}")
+
+
+def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: int | None = None):
+    """Time the C oracle (restatement of Go hash/crc32 slicing-by-8 as called by
+    ethernet/crc.go:19-21) on a bounded sample of the same frames."""
+    from oracle import oracle as O
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    nsamp = min(len(off_np) - 1, 1 << 16)
+    sample_bytes = int(off_np[nsamp] - off_np[0])
+    host = d_bytes[int(off_np[0]):int(off_np[nsamp])].cpu().numpy()
+    off_s = (off_np[:nsamp + 1] - off_np[0]).astype(np.uint64)
+    res = {}
+    for t in sorted({1, threads}):
+        O.crc32_frames(host, off_s, threads=t)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.crc32_frames(host, off_s, threads=t)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s / 2:
+                break
+        res[t] = reps * sample_bytes / el / 2**30
+    return {
+        "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "value_1core": round(res[1], 3),
+        "sample": f"{nsamp} frames x {frame_len or 'zipf'} B ({sample_bytes/1e6:.0f} MB) of the same synthetic batch, "
+                  f"repeated for ~{budget_s/2:.0f}s per thread count; C restatement of Go hash/crc32 "
+                  f"(slicing-by-8), NOT lneto's Go binary (no Go toolchain on the box)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="auto",
+                    choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
+    ap.add_argument("--verify", action="store_true", help="spot-check results against the oracle")
+    args = ap.parse_args()
+
+    import torch
+    import lneto_amd as L
+    from lneto_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    wname, n_rank, flen, desc = workload_spec(args.workload, world)
+    # Frame index slice of this rank within the global batch (weak scaling:
+    # the global batch grows with N, every rank owns n_rank frames).
+    n_total = n_rank * world
+    lo, hi = shard_range(n_total, world, rank)
+    n_local = hi - lo
+    if flen is None:
+        lens = synth.zipf_lengths(n_local, seed=synth.ZIPF_SEED + rank)
+        off_np = synth.offsets_from_lengths(lens)
+    else:
+        off_np = synth.fixed_offsets(n_local, flen)
+    nbytes = int(off_np[-1])
+    d_bytes = synth.bytes_torch(nbytes, dev, seed=synth.SEED + lo * 0x10001)
+    d_off = torch.from_numpy(off_np.astype(np.int64)).to(dev)
+    d_crc = torch.empty(n_local, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        starts[k].record(stream)
+        step()
+        ends[k].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max, kern_ms_max = float(t[0]), float(t[1])
+    total_bytes = nbytes * world  # every rank owns the same byte count (fixed-size frames)
+    if dist and flen is None:
+        tb = torch.tensor([nbytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(tb)
+        total_bytes = int(tb.item())
+
+    value = total_bytes * args.steps / elapsed_max / 2**30
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9  # GB/s, this rank's launches, HIP-event timed
+
+    out = {
+        "metric": "GiB/s CRC-32 over device-resident 1500B frames; % of HBM3E read peak",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 counter-hash bytes, generated on device)",
+        "config": {
+            "workload": desc,
+            "name": wname,
+            "frames_per_gpu": n_local,
+            "frame_bytes": flen if flen else "zipf 64-1500",
+            "bytes_per_gpu": nbytes,
+            "parallelism": f"per-GPU frame partition x{world} (no collective)",
+            "kernel": L.version(),
+        },
+        "pct_hbm_peak": round(100.0 * (nbytes / (elapsed_max / args.steps) / 1e9) / HBM_PEAK_GBS, 2),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "lnx::crc32_frames_kernel<kCrc>",
+            "kernel_ms": round(kern_ms, 4),
+            "algorithmic_bytes_per_launch": nbytes,
+        },
+    }
+    traffic_file = os.path.join(ROOT, "profiles", f"traffic_{wname}.json")
+    if os.path.exists(traffic_file):
+        with open(traffic_file) as fh:
+            tr = json.load(fh)
+        out["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+        out["roofline"]["traffic_source"] = os.path.relpath(traffic_file, ROOT)
+
+    if args.verify:
+        from oracle import oracle as O
+        idx = np.random.default_rng(rank).choice(n_local, min(256, n_local), replace=False)
+        got = d_crc.cpu().numpy().view(np.uint32)
+        for i in idx:
+            s, e = int(off_np[i]), int(off_np[i + 1])
+            assert int(got[i]) == O.crc32(d_bytes[s:e].cpu().numpy().tobytes()), f"mismatch frame {i}"
+        out["verified_sample"] = len(idx)
+
+    if args.with_copies and rank == 0:
+        host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        host.copy_(d_bytes)
+        hcrc = torch.empty(n_local, dtype=torch.int32, pin_memory=True)
+        d2 = torch.empty_like(d_bytes)
+        torch.cuda.synchronize(dev)
+        reps = 5
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            d2.copy_(host, non_blocking=True)
+            L.crc32_batch(d2, d_off, out=d_crc, stream=stream)
+            hcrc.copy_(d_crc, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t1) / reps
+        out["pcie_inclusive"] = {"value": round(nbytes / el / 2**30, 2), "unit": "GiB/s",
+                                 "note": "pinned H2D of frames + kernel + D2H of CRCs, serial, 1 stream"}
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

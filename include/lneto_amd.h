@@ -1,0 +1,137 @@
+/*
+ * lneto_amd.h — C-ABI of the MI355X-native checksum path of lneto.
+ *
+ * Scope: the IEEE 802.3 CRC-32 frame-check-sequence
+ * (lneto ethernet/crc.go) and the RFC 791 16-bit one's-complement internet
+ * checksum (lneto crc.go, type CRC791).  Everything here is integer / byte
+ * arithmetic and bit-identical to the reference.
+ *
+ * Two families of entry points:
+ *
+ *  1. Per-frame, host-CPU, exact Go semantics.  These back the drop-in
+ *     replacements of the reference's single-frame functions and NEVER launch
+ *     a GPU kernel (a launch costs microseconds, a 64-byte CRC costs tens of
+ *     nanoseconds; SURVEY.md §7 "cgo/HIP boundary").
+ *
+ *  2. Batched, device-resident, HIP kernels for gfx950.  Frames are packed back
+ *     to back in one device buffer and described by N+1 uint64 byte offsets:
+ *     frame i is bytes[off[i] : off[i+1]].  These are the hot path.
+ *
+ * Conventions (mirroring the reference):
+ *  - the caller owns every buffer; nothing is retained after a call returns;
+ *  - batch entry points return LNX_OK (0) or a negative LNX_E* code and never
+ *    abort; per-frame checksum functions return values, never errors;
+ *  - `stream` is a hipStream_t passed as an opaque pointer (NULL = the null
+ *    stream of the current device); batch calls are asynchronous on it.
+ */
+#ifndef LNETO_AMD_H
+#define LNETO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define LNX_OK 0
+#define LNX_EINVAL (-1)    /* bad argument (NULL pointer with n > 0, ...) */
+#define LNX_ENODEV (-2)    /* no HIP device / bad device ordinal */
+#define LNX_EHIP (-3)      /* a HIP runtime call failed; see lnx_last_error() */
+#define LNX_ENOMEM (-5)
+
+/* CRC-32/ISO-HDLC residue: CRC32(frame || LE32(CRC32(frame))) == this value. */
+#define LNX_CRC32_RESIDUE 0x2144DF1Cu
+
+/* ======================================================================== *
+ * 1. Per-frame host functions (exact Go semantics, never touch the GPU)
+ * ======================================================================== */
+
+/* Go: crc32.Update(crc, crc32.IEEETable, p) — the CRC32Update plugin hook
+ * type of internet.StackEthernetConfig (internet/stack-ethernet.go:31-32),
+ * surfaced as xnet.StackConfig.EthernetTxCRC32Update (x/xnet/stack-async.go:89)
+ * and called at internet/stack-ethernet.go:211-214. */
+uint32_t lnx_crc32_update(uint32_t crc, const uint8_t* p, size_t n);
+
+/* Go: ethernet.CRC32(data) (ethernet/crc.go:19-21). CRC32(nil) == 0. */
+uint32_t lnx_crc32(const uint8_t* p, size_t n);
+
+/* Go: ethernet.CRC32Search(data, minOffCRC) (ethernet/crc.go:28-47).
+ * First off >= max(minOff,0) with CRC32(data[:off]) == LE32(data[off:]),
+ * or -1. */
+int64_t lnx_crc32_search(const uint8_t* p, size_t n, int64_t min_off);
+
+/* Go: sumWriteEven (crc.go:23-28) — uint32 wrap-around sum of big-endian
+ * 16-bit words.  n must be even (the Go method panics on odd length, crc.go:30);
+ * here an odd trailing byte is ignored and the caller is expected not to pass one. */
+uint32_t lnx_sum_write_even(uint32_t sum, const uint8_t* p, size_t n);
+
+/* Go: sum16 (crc.go:17-21) — CRC791.Sum16() of a running sum. */
+uint16_t lnx_sum16(uint32_t sum);
+
+/* Go: CRC791{sum}.PayloadSum16(p) (crc.go:52-59). */
+uint16_t lnx_sum16_payload(uint32_t sum, const uint8_t* p, size_t n);
+
+/* Go: lneto.NeverZeroSum (crc.go:65-71). */
+uint16_t lnx_never_zero_sum(uint16_t sum16);
+
+/* ======================================================================== *
+ * 2. Batched device-resident HIP path (gfx950)
+ * ======================================================================== */
+
+/* d_crc[i] = CRC32(d_bytes[d_off[i] : d_off[i+1]]) for i in [0, n).
+ * d_off holds n+1 non-decreasing offsets (a frame whose end offset is below
+ * its start is treated as empty); frames may have any length and any byte
+ * alignment.  Replaces n calls of
+ * ethernet.CRC32 (ethernet/crc.go:19-21) / of the CRC32Update hook with crc=0
+ * (internet/stack-ethernet.go:211-214). */
+int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n,
+                    uint32_t* d_crc, void* stream);
+
+/* FCS verify of received frames that still carry their 4-byte LE FCS:
+ * d_ok[i] = 1 iff len_i >= 4 and CRC32(f[:len_i-4]) == LE32(f[len_i-4:]),
+ * evaluated as the residue test CRC32(f) == LNX_CRC32_RESIDUE.  This is the
+ * check lneto leaves to the PHY (x/netdev/interface.go:34-40) and would do at
+ * netdev.Stack.IngressPackets (x/netdev/interface.go:89) — SURVEY.md §8(f).1. */
+int lnx_fcs_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n,
+                         uint8_t* d_ok, void* stream);
+
+/* Internet checksum of n segments: d_out[i] = CRC791{d_seed[i]}.PayloadSum16(
+ * d_bytes[d_off[i] : d_off[i] + d_len[i]])  (crc.go:52-59).  d_seed may be
+ * NULL (all-zero seeds).  The seed is the pseudo-header partial sum written by
+ * ipv4.Frame.CRCWriteTCPPseudo / CRCWriteUDPPseudo (ipv4/frame.go:154-170) or
+ * ipv6.Frame.CRCWritePseudo (ipv6/frame.go:104-108). */
+int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                    const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream);
+
+/* Host-memory convenience: copies h_bytes/h_off to the device, runs
+ * lnx_crc32_batch, copies the CRCs back, synchronously.  Used to measure the
+ * PCIe-inclusive rate.  nbytes is the length of h_bytes; every
+ * offset must be <= nbytes. `device` is the HIP device ordinal. */
+int lnx_crc32_batch_host(const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_off,
+                         uint64_t n, uint32_t* h_crc, int device);
+
+/* Multi-GPU: the frame index range [0, n) is split into ngpu contiguous
+ * slices, one host thread per device; device g computes its slice from its own
+ * copy of the data: d_bytes_per_gpu[g] / d_off_per_gpu[g] describe that
+ * device's frames (offsets local to its buffer), d_crc_per_gpu[g] receives
+ * its results.  No collective, no peer traffic. */
+int lnx_crc32_batch_multi(int ngpu, const int* devices, const uint8_t* const* d_bytes_per_gpu,
+                          const uint64_t* const* d_off_per_gpu, const uint64_t* n_per_gpu,
+                          uint32_t* const* d_crc_per_gpu);
+
+/* Number of visible HIP devices (0 when none). */
+int lnx_device_count(void);
+
+/* Human-readable description of the last LNX_EHIP failure on this thread. */
+const char* lnx_last_error(void);
+
+/* Library build identification (kernel variant, gfx target). */
+const char* lnx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LNETO_AMD_H */

@@ -1,0 +1,165 @@
+// lneto_amd.hpp — C++ host mirror of lneto's checksum API over the C-ABI.
+//
+// Same names, argument meaning and error behaviour as the Go reference, so a
+// C++ caller (and the C++ tests) read like lneto's own code:
+//
+//   Go (reference)                                   C++ (this header)
+//   ethernet.CRC32(data) uint32          crc.go:19   ethernet::CRC32(data)
+//   ethernet.CRC32Search(data, min) int  crc.go:28   ethernet::CRC32Search(data, min)
+//   crc32.Update(crc, IEEETable, p)      hook type   ethernet::CRC32Update (a CRC32UpdateFunc)
+//   lneto.CRC791{...}                    crc.go:13   lneto::CRC791
+//   lneto.NeverZeroSum                   crc.go:65   lneto::NeverZeroSum
+//   lneto.ErrBadCRC                      errors.go:10 lneto::Err::BadCRC
+//   ipv4.Frame.CRCWrite{Header,TCPPseudo,UDPPseudo}   ipv4::CRCWrite*
+//   ipv6.Frame.CRCWritePseudo                          ipv6::CRCWritePseudo
+//   internet.StackEthernetConfig{AppendCRC32,CRC32Update} + the FCS append of
+//   StackEthernet.Encapsulate (internet/stack-ethernet.go:203-215)
+//                                                      internet::AppendFCS
+//
+// Batch extensions (device-resident, HIP): ethernet::CRC32Batch,
+// ethernet::VerifyFCSBatch, lneto::PayloadSum16Batch.  They return LNX_OK or a
+// negative LNX_E* code (the Go side would wrap these into an error value).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "lneto_amd.h"
+
+namespace lneto {
+
+// Mirrors lneto's error convention for this path: a checksum mismatch makes
+// the caller drop the frame with ErrBadCRC (errors.go:10).
+enum class Err : int { None = 0, BadCRC = 3 };
+
+// Non-owning byte view (the Go []byte of the reference API).
+struct Bytes {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  Bytes() = default;
+  Bytes(const uint8_t* p_, size_t n_) : p(p_), n(n_) {}
+  Bytes(const std::vector<uint8_t>& v) : p(v.data()), n(v.size()) {}  // NOLINT
+  Bytes sub(size_t lo, size_t hi) const { return Bytes(p + lo, hi - lo); }
+};
+
+// lneto.CRC791 (crc.go:13-62).  The zero value is ready to use.
+struct CRC791 {
+  uint32_t sum = 0;
+  // Panics in Go on odd length (crc.go:30); here the trailing byte is ignored
+  // and callers must pass even lengths, as the reference requires.
+  void WriteEven(Bytes b) { sum = lnx_sum_write_even(sum, b.p, b.n); }
+  void AddUint32(uint32_t v) {
+    AddUint16(uint16_t(v >> 16));
+    AddUint16(uint16_t(v));
+  }
+  void AddUint16(uint16_t v) { sum += v; }
+  uint16_t Sum16() const { return lnx_sum16(sum); }
+  uint16_t PayloadSum16(Bytes b) const { return lnx_sum16_payload(sum, b.p, b.n); }
+  void Reset() { sum = 0; }
+};
+
+inline uint16_t NeverZeroSum(uint16_t s) { return lnx_never_zero_sum(s); }
+
+// Batch: out[i] = CRC791{seed[i]}.PayloadSum16(bytes[off[i] : off[i]+len[i]]) on the GPU.
+inline int PayloadSum16Batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                             const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream = nullptr) {
+  return lnx_sum16_batch(d_bytes, d_off, d_len, d_seed, n, d_out, stream);
+}
+
+}  // namespace lneto
+
+namespace ethernet {
+using lneto::Bytes;
+
+// The plugin-hook signature of StackEthernetConfig.CRC32Update
+// (internet/stack-ethernet.go:31-32): func(crc uint32, p []byte) uint32.
+using CRC32UpdateFunc = uint32_t (*)(uint32_t crc, const uint8_t* p, size_t n);
+
+// Go crc32.Update(crc, crc32.IEEETable, p): pass as CRC32Update.
+inline uint32_t CRC32Update(uint32_t crc, const uint8_t* p, size_t n) { return lnx_crc32_update(crc, p, n); }
+
+inline uint32_t CRC32(Bytes data) { return lnx_crc32(data.p, data.n); }
+
+inline int CRC32Search(Bytes data, int minOffCRC) {
+  return (int)lnx_crc32_search(data.p, data.n, minOffCRC);
+}
+
+// Batch extensions over packed frames (device pointers).
+inline int CRC32Batch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
+                      void* stream = nullptr) {
+  return lnx_crc32_batch(d_frames, d_off, n, d_crc, stream);
+}
+inline int VerifyFCSBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
+                          void* stream = nullptr) {
+  return lnx_fcs_verify_batch(d_frames, d_off, n, d_ok, stream);
+}
+
+}  // namespace ethernet
+
+namespace ipv4 {
+using lneto::Bytes;
+using lneto::CRC791;
+// ipv4/frame.go:144-146 — the header sum covers exactly 20 bytes (options are not covered).
+inline void CRCWriteHeader(Bytes ip, CRC791& c) { c.WriteEven(ip.sub(0, 20)); }
+// ipv4/frame.go:138-142
+inline uint16_t CalculateHeaderCRC(Bytes ip) {
+  CRC791 c;
+  CRCWriteHeader(ip, c);
+  return c.Sum16();
+}
+inline uint16_t TotalLength(Bytes ip) { return uint16_t(ip.p[2] << 8 | ip.p[3]); }
+inline uint8_t HeaderLength(Bytes ip) { return uint8_t((ip.p[0] & 0xF) * 4); }
+// ipv4/frame.go:154-158
+inline void CRCWriteTCPPseudo(Bytes ip, CRC791& c) {
+  c.WriteEven(ip.sub(12, 20));
+  c.AddUint16(uint16_t(TotalLength(ip) - HeaderLength(ip)));
+  c.AddUint16(ip.p[9]);
+}
+// ipv4/frame.go:166-170
+inline void CRCWriteUDPPseudo(Bytes ip, CRC791& c, uint16_t udpLength) {
+  c.WriteEven(ip.sub(12, 20));
+  c.AddUint16(udpLength);
+  c.AddUint16(ip.p[9]);
+}
+}  // namespace ipv4
+
+namespace ipv6 {
+using lneto::Bytes;
+using lneto::CRC791;
+// ipv6/frame.go:104-108
+inline void CRCWritePseudo(Bytes ip6, CRC791& c) {
+  c.WriteEven(ip6.sub(8, 40));
+  c.AddUint32(uint32_t(ip6.p[4] << 8 | ip6.p[5]));
+  c.AddUint32(ip6.p[6]);
+}
+}  // namespace ipv6
+
+namespace internet {
+// The CRC-related fields of StackEthernetConfig (internet/stack-ethernet.go:28-32).
+struct StackEthernetConfig {
+  bool AppendCRC32 = false;
+  ethernet::CRC32UpdateFunc CRC32Update = nullptr;
+};
+
+// Config validation of StackEthernet.Configure (internet/stack-ethernet.go:92-93):
+// AppendCRC32 without a CRC32Update is an invalid configuration.
+inline bool ValidCRCConfig(const StackEthernetConfig& c) { return !(c.AppendCRC32 && c.CRC32Update == nullptr); }
+
+// Tail of StackEthernet.Encapsulate (internet/stack-ethernet.go:203-215): pad the
+// frame to 60 bytes, then, if configured, append CRC32Update(0, frame) little-endian.
+// `frame` must have room for max(n, 60) + 4 bytes.  Returns the new length.
+inline size_t AppendFCS(uint8_t* frame, size_t n, const StackEthernetConfig& c) {
+  const size_t minFrameSize = 60;
+  while (n < minFrameSize) frame[n++] = 0;
+  if (c.CRC32Update != nullptr) {
+    const uint32_t crc = c.CRC32Update(0, frame, n);
+    frame[n] = uint8_t(crc);
+    frame[n + 1] = uint8_t(crc >> 8);
+    frame[n + 2] = uint8_t(crc >> 16);
+    frame[n + 3] = uint8_t(crc >> 24);
+    n += 4;
+  }
+  return n;
+}
+}  // namespace internet

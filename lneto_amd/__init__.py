@@ -1,0 +1,238 @@
+"""lneto_amd — MI355X-native batched checksum path of lneto.
+
+Python binding (ctypes) of the C-ABI in include/lneto_amd.h, implemented by
+lneto_amd/liblneto_amd.so (hand-written HIP kernels for gfx950 + host C++).
+PyTorch is used only as device-memory / stream plumbing for the batch calls.
+
+Mirrors the reference's API for this path:
+    ethernet.CRC32 / CRC32Search / crc32.Update   -> crc32, crc32_search, crc32_update
+    lneto.CRC791 / NeverZeroSum                   -> CRC791, never_zero_sum
+    batch (device-resident) extensions            -> crc32_batch, fcs_verify_batch, sum16_batch
+
+There is no CPU fallback for the batch calls: if the library is missing this
+module raises at import; if no HIP device is usable the batch calls raise
+LnetoError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+__all__ = [
+    "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
+    "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
+    "crc32_batch_host", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblneto_amd.so")
+CRC32_RESIDUE = 0x2144DF1C
+
+LNX_OK, LNX_EINVAL, LNX_ENODEV, LNX_EHIP, LNX_ENOMEM = 0, -1, -2, -3, -5
+_ERRNAMES = {LNX_EINVAL: "EINVAL", LNX_ENODEV: "ENODEV", LNX_EHIP: "EHIP", LNX_ENOMEM: "ENOMEM"}
+
+
+class LnetoError(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "or `make -C lneto_amd/csrc`")
+
+# PyTorch-ROCm bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1.  If this
+# library were loaded first it would pull /opt/rocm's copies in, and torch would
+# then load its bundled ones as well: two HSA runtimes in one process, and HIP
+# calls from one of them see no device.  Importing torch first makes the dynamic
+# linker resolve our libamdhip64.so.7 dependency to torch's already-loaded one,
+# so the process has exactly one HIP runtime.  (C / C++ / cgo users get /opt/rocm's.)
+try:
+    import torch as _torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is plumbing, not a dependency of the C-ABI
+    _torch = None
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_sig = {
+    "lnx_crc32_update": (ctypes.c_uint32, [ctypes.c_uint32, _u8p, ctypes.c_size_t]),
+    "lnx_crc32": (ctypes.c_uint32, [_u8p, ctypes.c_size_t]),
+    "lnx_crc32_search": (ctypes.c_int64, [_u8p, ctypes.c_size_t, ctypes.c_int64]),
+    "lnx_sum_write_even": (ctypes.c_uint32, [ctypes.c_uint32, _u8p, ctypes.c_size_t]),
+    "lnx_sum16": (ctypes.c_uint16, [ctypes.c_uint32]),
+    "lnx_sum16_payload": (ctypes.c_uint16, [ctypes.c_uint32, _u8p, ctypes.c_size_t]),
+    "lnx_never_zero_sum": (ctypes.c_uint16, [ctypes.c_uint16]),
+    "lnx_crc32_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_fcs_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_sum16_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
+    "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "lnx_device_count": (ctypes.c_int, []),
+    "lnx_last_error": (ctypes.c_char_p, []),
+    "lnx_version": (ctypes.c_char_p, []),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != LNX_OK:
+        detail = lib.lnx_last_error().decode() if rc == LNX_EHIP else ""
+        raise LnetoError(f"{what} failed: {_ERRNAMES.get(rc, rc)} {detail}".strip())
+
+
+def _buf(data: bytes):
+    data = bytes(data)
+    return (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(data or b"\0"), len(data)
+
+
+# ----------------------------------------------------------- per-frame (host)
+def crc32_update(crc: int, p: bytes) -> int:
+    """Go crc32.Update(crc, IEEETable, p) — the CRC32Update hook (internet/stack-ethernet.go:31-32)."""
+    b, n = _buf(p)
+    return lib.lnx_crc32_update(crc & 0xFFFFFFFF, b, n)
+
+
+def crc32(p: bytes) -> int:
+    """ethernet.CRC32 (ethernet/crc.go:19-21)."""
+    b, n = _buf(p)
+    return lib.lnx_crc32(b, n)
+
+
+def crc32_search(p: bytes, min_off: int) -> int:
+    """ethernet.CRC32Search (ethernet/crc.go:28-47)."""
+    b, n = _buf(p)
+    return lib.lnx_crc32_search(b, n, min_off)
+
+
+def sum_write_even(s: int, p: bytes) -> int:
+    if len(p) & 1:
+        raise IndexError("WriteEven requires an even-length buffer (crc.go:30)")
+    b, n = _buf(p)
+    return lib.lnx_sum_write_even(s & 0xFFFFFFFF, b, n)
+
+
+def sum16(s: int) -> int:
+    return lib.lnx_sum16(s & 0xFFFFFFFF)
+
+
+def payload_sum16(s: int, p: bytes) -> int:
+    b, n = _buf(p)
+    return lib.lnx_sum16_payload(s & 0xFFFFFFFF, b, n)
+
+
+def never_zero_sum(x: int) -> int:
+    return lib.lnx_never_zero_sum(x & 0xFFFF)
+
+
+class CRC791:
+    """lneto.CRC791 (crc.go:13-62): running RFC 791 one's-complement sum."""
+
+    __slots__ = ("sum",)
+
+    def __init__(self) -> None:
+        self.sum = 0
+
+    def WriteEven(self, buff: bytes) -> None:
+        self.sum = sum_write_even(self.sum, buff)
+
+    def AddUint16(self, v: int) -> None:
+        self.sum = (self.sum + (v & 0xFFFF)) & 0xFFFFFFFF
+
+    def AddUint32(self, v: int) -> None:
+        self.AddUint16((v >> 16) & 0xFFFF)
+        self.AddUint16(v & 0xFFFF)
+
+    def Sum16(self) -> int:
+        return sum16(self.sum)
+
+    def PayloadSum16(self, buff: bytes) -> int:
+        return payload_sum16(self.sum, buff)
+
+    def Reset(self) -> None:
+        self.sum = 0
+
+
+# ------------------------------------------------------- batched (device)
+def _stream_ptr(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _dev_check(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda or not t.is_contiguous()):
+            raise LnetoError("batch arguments must be contiguous device tensors")
+
+
+def crc32_batch(d_bytes, d_off, out=None, stream=None):
+    """CRC32 of every frame d_bytes[d_off[i]:d_off[i+1]] on the GPU.
+
+    d_bytes: uint8 device tensor; d_off: int64 device tensor of N+1 offsets.
+    Returns an int32 device tensor holding the uint32 CRCs bit-for-bit.
+    """
+    import torch
+    _dev_check(d_bytes, d_off)
+    n = d_off.numel() - 1
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int32, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_crc32_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
+                                   _stream_ptr(stream)), "lnx_crc32_batch")
+    return out
+
+
+def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
+    """1 where frame i (payload + trailing LE FCS) passes the FCS check, else 0."""
+    import torch
+    _dev_check(d_bytes, d_off)
+    n = d_off.numel() - 1
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.uint8, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
+                                        _stream_ptr(stream)), "lnx_fcs_verify_batch")
+    return out
+
+
+def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):
+    """CRC791{seed[i]}.PayloadSum16(d_bytes[off[i]:off[i]+len[i]]) on the GPU.
+
+    d_off: int64 (N), d_len: int32 (N), d_seed: int32 (N) or None.  Returns int16 (uint16 bits).
+    """
+    import torch
+    _dev_check(d_bytes, d_off, d_len, d_seed)
+    n = d_off.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_sum16_batch(d_bytes.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                   d_seed.data_ptr() if d_seed is not None else None, n,
+                                   out.data_ptr(), _stream_ptr(stream)), "lnx_sum16_batch")
+    return out
+
+
+def crc32_batch_host(h_bytes, h_off, device: int = 0):
+    """Host-memory convenience (H2D + kernel + D2H); numpy uint8 / uint64 in, uint32 out."""
+    import numpy as np
+    h_bytes = np.ascontiguousarray(h_bytes, dtype=np.uint8)
+    h_off = np.ascontiguousarray(h_off, dtype=np.uint64)
+    n = len(h_off) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    if n > 0:
+        _check(lib.lnx_crc32_batch_host(h_bytes.ctypes.data, h_bytes.nbytes, h_off.ctypes.data, n,
+                                        out.ctypes.data, device), "lnx_crc32_batch_host")
+    return out[:max(n, 0)]
+
+
+def device_count() -> int:
+    return lib.lnx_device_count()
+
+
+def version() -> str:
+    return lib.lnx_version().decode()

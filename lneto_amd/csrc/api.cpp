@@ -1,0 +1,199 @@
+// api.cpp — C-ABI of the batched HIP path: per-device context (the LDS table
+// image), argument checks, host-memory and multi-GPU conveniences.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+#include "../../include/lneto_amd.h"
+#include "gf2.hpp"
+#include "lds_layout.hpp"
+
+namespace lnx {
+hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
+                               bool verify, const void* image, int num_cus, hipStream_t stream);
+hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
+                                 const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
+                                 hipStream_t stream);
+
+// The 160 KiB LDS image (lds_layout.hpp), built once on the host.
+std::vector<uint32_t> build_lds_image() {
+  std::vector<uint32_t> img(kLdsDwords, 0);
+  for (uint32_t m = 0; m < 4; ++m) {
+    for (uint32_t e = 0; e < 256; ++e) {
+      const uint32_t v = zshift_bytes(e << (8 * m), kWindowBytes);  // U_m[e] = Z_256(e << 8m)
+      for (uint32_t c = 0; c < 32; ++c) img[u_addr(m, e, c) / 4] = v;
+    }
+  }
+  for (uint32_t lane = 0; lane < 64; ++lane) {
+    for (uint32_t i = 0; i < 8; ++i) {
+      for (uint32_t v = 0; v < 16; ++v) {
+        img[f_addr(lane, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * (int64_t)lane);  // F_l = Z_{-4l}
+      }
+    }
+  }
+  return img;
+}
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return LNX_EHIP;
+}
+
+struct DeviceCtx {
+  std::once_flag once;
+  int status = LNX_OK;
+  void* d_image = nullptr;
+  int num_cus = 0;
+};
+
+constexpr int kMaxDevices = 64;
+DeviceCtx g_ctx[kMaxDevices];
+
+const std::vector<uint32_t>& host_image() {
+  static const std::vector<uint32_t> img = build_lds_image();
+  return img;
+}
+
+// Context of the calling thread's current device (created on first use).
+int get_ctx(DeviceCtx** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev < 0 || dev >= kMaxDevices) return LNX_ENODEV;
+  DeviceCtx& c = g_ctx[dev];
+  std::call_once(c.once, [&] {
+    hipError_t err = hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipDeviceGetAttribute"); return; }
+    const auto& img = host_image();
+    err = hipMalloc(&c.d_image, img.size() * 4);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(image)"); return; }
+    err = hipMemcpy(c.d_image, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(image)"); return; }
+  });
+  if (c.status != LNX_OK) return c.status;
+  *out = &c;
+  return LNX_OK;
+}
+
+int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify,
+               void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_out) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
+                                     static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32_frames_kernel launch");
+  return LNX_OK;
+}
+
+}  // namespace
+}  // namespace lnx
+
+using namespace lnx;
+
+extern "C" {
+
+int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
+                    void* stream) {
+  return crc_common(d_bytes, d_off, n, d_crc, false, stream);
+}
+
+int lnx_fcs_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
+                         void* stream) {
+  return crc_common(d_bytes, d_off, n, d_ok, true, stream);
+}
+
+int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                    const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_len || !d_out) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_sum16_segments(d_bytes, d_off, d_len, d_seed, n, d_out, c->num_cus,
+                                       static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "sum16_segments_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_crc32_batch_host(const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_off, uint64_t n,
+                         uint32_t* h_crc, int device) {
+  if (n == 0) return LNX_OK;
+  if (!h_bytes || !h_off || !h_crc) return LNX_EINVAL;
+  for (uint64_t i = 0; i <= n; ++i)
+    if (h_off[i] > nbytes) return LNX_EINVAL;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  uint8_t* d_bytes = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_crc = nullptr;
+  int rc = LNX_OK;
+  hipStream_t s = nullptr;
+  if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  if ((e = hipMallocAsync(reinterpret_cast<void**>(&d_bytes), nbytes ? nbytes : 4, s)) != hipSuccess ||
+      (e = hipMallocAsync(reinterpret_cast<void**>(&d_off), (n + 1) * 8, s)) != hipSuccess ||
+      (e = hipMallocAsync(reinterpret_cast<void**>(&d_crc), n * 4, s)) != hipSuccess) {
+    rc = hip_fail(e, "hipMallocAsync");
+  }
+  if (rc == LNX_OK) {
+    if ((e = hipMemcpyAsync(d_bytes, h_bytes, nbytes, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_off, h_off, (n + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+      rc = hip_fail(e, "hipMemcpyAsync H2D");
+  }
+  if (rc == LNX_OK) rc = lnx_crc32_batch(d_bytes, d_off, n, d_crc, s);
+  if (rc == LNX_OK && (e = hipMemcpyAsync(h_crc, d_crc, n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    rc = hip_fail(e, "hipMemcpyAsync D2H");
+  if (d_bytes) (void)hipFreeAsync(d_bytes, s);
+  if (d_off) (void)hipFreeAsync(d_off, s);
+  if (d_crc) (void)hipFreeAsync(d_crc, s);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess && rc == LNX_OK) rc = hip_fail(e, "hipStreamSynchronize");
+  (void)hipStreamDestroy(s);
+  return rc;
+}
+
+int lnx_crc32_batch_multi(int ngpu, const int* devices, const uint8_t* const* d_bytes_per_gpu,
+                          const uint64_t* const* d_off_per_gpu, const uint64_t* n_per_gpu,
+                          uint32_t* const* d_crc_per_gpu) {
+  if (ngpu <= 0 || !devices || !d_bytes_per_gpu || !d_off_per_gpu || !n_per_gpu || !d_crc_per_gpu)
+    return LNX_EINVAL;
+  std::vector<int> rcs(ngpu, LNX_OK);
+  std::vector<std::string> errs(ngpu);
+  std::vector<std::thread> th;
+  for (int g = 0; g < ngpu; ++g) {
+    th.emplace_back([&, g] {
+      hipError_t e = hipSetDevice(devices[g]);
+      if (e != hipSuccess) { rcs[g] = hip_fail(e, "hipSetDevice"); errs[g] = g_last_error; return; }
+      int rc = lnx_crc32_batch(d_bytes_per_gpu[g], d_off_per_gpu[g], n_per_gpu[g], d_crc_per_gpu[g], nullptr);
+      if (rc == LNX_OK && (e = hipDeviceSynchronize()) != hipSuccess) rc = hip_fail(e, "hipDeviceSynchronize");
+      rcs[g] = rc;
+      if (rc != LNX_OK) errs[g] = g_last_error;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < ngpu; ++g)
+    if (rcs[g] != LNX_OK) { g_last_error = errs[g]; return rcs[g]; }
+  return LNX_OK;
+}
+
+int lnx_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* lnx_last_error(void) { return g_last_error.c_str(); }
+
+const char* lnx_version(void) {
+  return "lneto_amd 0.1 gfx950: crc32 wave-per-frame/lane-private-LDS-U256 + sum16 wave-per-segment";
+}
+
+}  // extern "C"

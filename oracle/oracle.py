@@ -1,0 +1,246 @@
+"""CPU oracle for lneto's checksum path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / the timed CPU baseline.  The product
+(lneto_amd/) never imports it.
+
+Two independent restatements live here:
+
+* pure-Python / zlib (this file):
+    - crc32 / crc32_update  == Go crc32.Checksum / crc32.Update(IEEETable)
+      (lneto ethernet/crc.go:13,19-21,36,44).  zlib.crc32 implements the same
+      CRC-32/ISO-HDLC algorithm as Go's hash/crc32 (stdlib dependency, not in
+      the reference tree; go.mod:3 floor go1.24, CI go1.26 ci.yaml:109).
+    - crc32_search          == ethernet/crc.go:28-47
+    - sum_write_even / sum16 / payload_sum16 / never_zero_sum == crc.go:17-71
+    - ipv4_* / ipv6_* pseudo-header seeds == ipv4/frame.go:138-170,
+      ipv6/frame.go:104-108
+* C (oracle/crc_oracle.c, built to oracle/liboracle.so), used for speed and as
+  the bench's CPU baseline ("port").
+
+Pinning: tests/test_oracle.py checks both against the reference's own
+known-answer vectors (lneto_test.go:119-160 IPv4/TCP sums; ethernet/crc_test.go
+self-consistency cases) and against the CRC-32/ISO-HDLC check value.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+CRC32_CHECK = 0xCBF43926   # CRC-32/ISO-HDLC of b"123456789"
+CRC32_RESIDUE = 0x2144DF1C  # CRC32(m || LE32(CRC32(m))) for every m
+
+
+# --------------------------------------------------------------------------- CRC-32
+def crc32_update(crc: int, p: bytes) -> int:
+    """Go crc32.Update(crc, crc32.IEEETable, p)."""
+    return zlib.crc32(bytes(p), crc) & 0xFFFFFFFF
+
+
+def crc32(p: bytes) -> int:
+    """ethernet.CRC32 (ethernet/crc.go:19-21)."""
+    return zlib.crc32(bytes(p)) & 0xFFFFFFFF
+
+
+def crc32_bitwise(p: bytes, crc: int = 0) -> int:
+    """Bit-serial CRC-32/ISO-HDLC (third restatement, small inputs only)."""
+    c = (~crc) & 0xFFFFFFFF
+    for b in bytes(p):
+        c ^= b
+        for _ in range(8):
+            c = (c >> 1) ^ (0xEDB88320 if c & 1 else 0)
+    return (~c) & 0xFFFFFFFF
+
+
+def crc32_search(data: bytes, min_off: int) -> int:
+    """ethernet.CRC32Search (ethernet/crc.go:28-47)."""
+    if min_off < 0:
+        min_off = 0
+    if len(data) < min_off + 4:
+        return -1
+    c = crc32(data[:min_off])
+    for off in range(min_off, len(data) - 3):
+        got = struct.unpack_from("<I", data, off)[0]
+        if c == got:
+            return off
+        c = crc32_update(c, data[off:off + 1])
+    return -1
+
+
+# ------------------------------------------------------------------ RFC 791 sum
+def sum_write_even(s: int, buff: bytes) -> int:
+    """sumWriteEven (crc.go:23-28): uint32 wrap-around add of BE16 words."""
+    for i in range(0, len(buff) - 1, 2):
+        s = (s + ((buff[i] << 8) | buff[i + 1])) & 0xFFFFFFFF
+    return s
+
+
+def sum16(s: int) -> int:
+    """sum16 (crc.go:17-21)."""
+    s = (s & 0xFFFF) + (s >> 16)
+    return (~(s + (s >> 16))) & 0xFFFF
+
+
+def payload_sum16(s: int, buff: bytes) -> int:
+    """(*CRC791).PayloadSum16 (crc.go:52-59), receiver sum = s."""
+    odd = len(buff) & 1
+    s = sum_write_even(s, buff[:len(buff) - odd])
+    if odd:
+        s = (s + (buff[-1] << 8)) & 0xFFFFFFFF
+    return sum16(s)
+
+
+def never_zero_sum(x: int) -> int:
+    """NeverZeroSum (crc.go:65-71)."""
+    return 0xFFFF if x == 0 else x
+
+
+class CRC791:
+    """Restatement of lneto.CRC791 (crc.go:13-62)."""
+
+    def __init__(self) -> None:
+        self.sum = 0
+
+    def write_even(self, buff: bytes) -> None:
+        if len(buff) & 1:
+            raise IndexError("WriteEven: odd length (crc.go:30 panics)")
+        self.sum = sum_write_even(self.sum, buff)
+
+    def add_uint16(self, v: int) -> None:
+        self.sum = (self.sum + (v & 0xFFFF)) & 0xFFFFFFFF
+
+    def add_uint32(self, v: int) -> None:
+        self.add_uint16(v >> 16)
+        self.add_uint16(v)
+
+    def sum16(self) -> int:
+        return sum16(self.sum)
+
+    def payload_sum16(self, buff: bytes) -> int:
+        return payload_sum16(self.sum, buff)
+
+    def reset(self) -> None:
+        self.sum = 0
+
+
+# ----------------------------------------------------- IPv4 / IPv6 pseudo-headers
+def ipv4_header_sum16(ip: bytes) -> int:
+    """ipv4.Frame.CalculateHeaderCRC (ipv4/frame.go:138-146): first 20 bytes only."""
+    c = CRC791()
+    c.write_even(ip[:20])
+    return c.sum16()
+
+
+def ipv4_tcp_pseudo(ip: bytes) -> CRC791:
+    """ipv4.Frame.CRCWriteTCPPseudo (ipv4/frame.go:154-158)."""
+    c = CRC791()
+    c.write_even(ip[12:20])
+    total_len = (ip[2] << 8) | ip[3]
+    ihl = (ip[0] & 0xF) * 4
+    c.add_uint16((total_len - ihl) & 0xFFFF)
+    c.add_uint16(ip[9])
+    return c
+
+
+def ipv4_udp_pseudo(ip: bytes, udp_length: int) -> CRC791:
+    """ipv4.Frame.CRCWriteUDPPseudo (ipv4/frame.go:166-170)."""
+    c = CRC791()
+    c.write_even(ip[12:20])
+    c.add_uint16(udp_length)
+    c.add_uint16(ip[9])
+    return c
+
+
+def ipv6_pseudo(ip6: bytes) -> CRC791:
+    """ipv6.Frame.CRCWritePseudo (ipv6/frame.go:104-108)."""
+    c = CRC791()
+    c.write_even(ip6[8:40])
+    c.add_uint32((ip6[4] << 8) | ip6[5])
+    c.add_uint32(ip6[6])
+    return c
+
+
+# ----------------------------------------------------------------- C oracle
+_lib = None
+
+
+def lib():
+    """ctypes handle of oracle/liboracle.so (built by `make -C oracle`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C oracle`")
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oracle_crc32.restype = ctypes.c_uint32
+        L.oracle_crc32.argtypes = [u8p, ctypes.c_size_t]
+        L.oracle_crc32_update.restype = ctypes.c_uint32
+        L.oracle_crc32_update.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.oracle_crc32_update_simple.restype = ctypes.c_uint32
+        L.oracle_crc32_update_simple.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.oracle_crc32_search.restype = ctypes.c_int64
+        L.oracle_crc32_search.argtypes = [u8p, ctypes.c_size_t, ctypes.c_int64]
+        L.oracle_payload_sum16.restype = ctypes.c_uint16
+        L.oracle_payload_sum16.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.oracle_crc32_frames.restype = ctypes.c_int
+        L.oracle_crc32_frames.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.c_void_p, ctypes.c_int]
+        L.oracle_sum16_segments.restype = None
+        L.oracle_sum16_segments.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _u8p(b: bytes):
+    buf = (ctypes.c_uint8 * max(len(b), 1)).from_buffer_copy(bytes(b) if len(b) else b"\0")
+    return buf
+
+
+def c_crc32(p: bytes) -> int:
+    return lib().oracle_crc32(_u8p(p), len(p))
+
+
+def c_crc32_simple(p: bytes, crc: int = 0) -> int:
+    return lib().oracle_crc32_update_simple(crc, _u8p(p), len(p))
+
+
+def c_crc32_search(p: bytes, min_off: int) -> int:
+    return lib().oracle_crc32_search(_u8p(p), len(p), min_off)
+
+
+def c_payload_sum16(seed: int, p: bytes) -> int:
+    return lib().oracle_payload_sum16(seed, _u8p(p), len(p))
+
+
+def crc32_frames(data: np.ndarray, off: np.ndarray, threads: int = 1) -> np.ndarray:
+    """CRC32 of every frame data[off[i]:off[i+1]] (C oracle, `threads` threads)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    n = len(off) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    lib().oracle_crc32_frames(data.ctypes.data, off.ctypes.data, n, out.ctypes.data, threads)
+    return out[:n]
+
+
+def sum16_segments(data: np.ndarray, off: np.ndarray, length: np.ndarray,
+                   seed: np.ndarray | None) -> np.ndarray:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    n = len(off)
+    out = np.zeros(max(n, 1), dtype=np.uint16)
+    sp = None
+    if seed is not None:
+        seed = np.ascontiguousarray(seed, dtype=np.uint32)
+        sp = seed.ctypes.data
+    lib().oracle_sum16_segments(data.ctypes.data, off.ctypes.data, length.ctypes.data, sp, n,
+                                out.ctypes.data)
+    return out[:n]

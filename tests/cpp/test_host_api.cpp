@@ -1,0 +1,119 @@
+// C++ mirror of lneto's own checksum tests, run against include/lneto_amd.hpp:
+//   ethernet/crc_test.go:8-100   TestCRC32Search
+//   lneto_test.go:119-160        TestIPv4TCPChecksum
+// plus the FCS-append tail of StackEthernet.Encapsulate (internet/stack-ethernet.go:203-215).
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "lneto_amd.hpp"
+
+static int failures = 0;
+#define EXPECT(cond, ...)                      \
+  do {                                         \
+    if (!(cond)) {                             \
+      std::printf("FAIL %s:%d ", __FILE__, __LINE__); \
+      std::printf(__VA_ARGS__);                \
+      std::printf("\n");                       \
+      ++failures;                              \
+    }                                          \
+  } while (0)
+
+static std::vector<uint8_t> makeDataWithCRC(int payloadLen) {  // crc_test.go:10-18
+  std::vector<uint8_t> data(payloadLen + 4);
+  for (int i = 0; i < payloadLen; ++i) data[i] = uint8_t(i);
+  uint32_t crc = ethernet::CRC32(lneto::Bytes(data.data(), payloadLen));
+  std::memcpy(&data[payloadLen], &crc, 4);  // little-endian host
+  return data;
+}
+
+static void TestCRC32Search() {
+  {
+    auto d = makeDataWithCRC(100);
+    EXPECT(ethernet::CRC32Search(d, 0) == 100, "finds CRC at end");
+    EXPECT(ethernet::CRC32Search(d, 50) == 100, "minOff before CRC");
+    EXPECT(ethernet::CRC32Search(d, 100) == 100, "minOff exactly at CRC");
+    EXPECT(ethernet::CRC32Search(d, 101) == -1, "minOff past CRC");
+  }
+  {
+    std::vector<uint8_t> d(100);
+    for (int i = 0; i < 100; ++i) d[i] = uint8_t(i);
+    EXPECT(ethernet::CRC32Search(d, 0) == -1, "no valid CRC");
+  }
+  {
+    std::vector<uint8_t> d = {1, 2, 3};
+    EXPECT(ethernet::CRC32Search(d, 0) == -1, "data too short");
+  }
+  {
+    auto d = makeDataWithCRC(20);
+    EXPECT(ethernet::CRC32Search(d, -5) == 20, "negative minOff");
+  }
+  {
+    std::vector<uint8_t> d(4);
+    uint32_t crc = ethernet::CRC32(lneto::Bytes());
+    std::memcpy(d.data(), &crc, 4);
+    EXPECT(ethernet::CRC32Search(d, 0) == 0, "CRC at position 0");
+  }
+  {
+    auto d = makeDataWithCRC(50);
+    d.resize(d.size() + 50, 0);
+    EXPECT(ethernet::CRC32Search(d, 0) == 50, "first valid CRC wins");
+  }
+}
+
+static void TestIPv4TCPChecksum() {
+  const uint8_t pkts[2][74] = {
+      {0xc0, 0xff, 0xee, 0x00, 0xde, 0xad, 0x4e, 0x8b, 0x3a, 0xf9, 0xfb, 0x6b, 0x08, 0x00, 0x45, 0x00,
+       0x00, 0x3c, 0x01, 0xbe, 0x40, 0x00, 0x40, 0x06, 0xa3, 0xaa, 0xc0, 0xa8, 0x0a, 0x01, 0xc0, 0xa8,
+       0x0a, 0x02, 0xe7, 0x0a, 0x00, 0x50, 0x40, 0x60, 0xd5, 0xcc, 0x00, 0x00, 0x00, 0x00, 0xa0, 0x02,
+       0xfa, 0xf0, 0x62, 0xbc, 0x00, 0x00, 0x02, 0x04, 0x05, 0xb4, 0x04, 0x02, 0x08, 0x0a, 0xbb, 0xac,
+       0x9b, 0xca, 0x00, 0x00, 0x00, 0x00, 0x01, 0x03, 0x03, 0x07},
+      {0xc0, 0xff, 0xee, 0x00, 0xde, 0xad, 0x4e, 0x8b, 0x3a, 0xf9, 0xfb, 0x6b, 0x08, 0x00, 0x45, 0x00,
+       0x00, 0x3c, 0xfa, 0xfd, 0x40, 0x00, 0x40, 0x06, 0xaa, 0x6a, 0xc0, 0xa8, 0x0a, 0x01, 0xc0, 0xa8,
+       0x0a, 0x02, 0xe7, 0x0e, 0x00, 0x50, 0x9c, 0xdc, 0xfe, 0x05, 0x00, 0x00, 0x00, 0x00, 0xa0, 0x02,
+       0xfa, 0xf0, 0xde, 0x02, 0x00, 0x00, 0x02, 0x04, 0x05, 0xb4, 0x04, 0x02, 0x08, 0x0a, 0xbb, 0xac,
+       0x9b, 0xca, 0x00, 0x00, 0x00, 0x00, 0x01, 0x03, 0x03, 0x07}};
+  for (const auto& p : pkts) {
+    std::vector<uint8_t> f(p, p + 74);
+    lneto::Bytes ip(f.data() + 14, f.size() - 14);
+    uint8_t* ipw = f.data() + 14;
+    uint16_t wantIP = uint16_t(ipw[10] << 8 | ipw[11]);
+    ipw[10] = ipw[11] = 0;  // zero the CRC field (lneto_test.go:143)
+    EXPECT(ipv4::CalculateHeaderCRC(ip) == wantIP, "IPv4 CRC want %x", wantIP);
+    uint8_t* tcp = ipw + 20;
+    uint16_t wantTCP = uint16_t(tcp[16] << 8 | tcp[17]);
+    lneto::CRC791 crc;
+    ipv4::CRCWriteTCPPseudo(ip, crc);
+    tcp[16] = tcp[17] = 0;  // lneto_test.go:153
+    uint16_t got = crc.PayloadSum16(lneto::Bytes(tcp, ipv4::TotalLength(ip) - ipv4::HeaderLength(ip)));
+    EXPECT(got == wantTCP, "TCP CRC want %x got %x", wantTCP, got);
+  }
+}
+
+static void TestAppendFCS() {
+  internet::StackEthernetConfig bad;
+  bad.AppendCRC32 = true;
+  EXPECT(!internet::ValidCRCConfig(bad), "AppendCRC32 without CRC32Update must be rejected");
+  internet::StackEthernetConfig cfg;
+  cfg.AppendCRC32 = true;
+  cfg.CRC32Update = ethernet::CRC32Update;
+  EXPECT(internet::ValidCRCConfig(cfg), "valid config");
+  std::vector<uint8_t> frame(64 + 4, 0);
+  for (int i = 0; i < 42; ++i) frame[i] = uint8_t(i * 7 + 1);  // a 42-byte runt (ARP-sized)
+  size_t n = internet::AppendFCS(frame.data(), 42, cfg);
+  EXPECT(n == 64, "padded to 60 + 4-byte FCS, got %zu", n);
+  EXPECT(ethernet::CRC32Search(lneto::Bytes(frame.data(), n), 0) == 60, "FCS found at 60");
+  EXPECT(ethernet::CRC32(lneto::Bytes(frame.data(), n)) == LNX_CRC32_RESIDUE, "residue");
+}
+
+int main() {
+  TestCRC32Search();
+  TestIPv4TCPChecksum();
+  TestAppendFCS();
+  if (failures) {
+    std::printf("%d failures\n", failures);
+    return 1;
+  }
+  std::printf("ok\n");
+  return 0;
+}

@@ -1,0 +1,70 @@
+"""The C-ABI library loads, exports every symbol include/lneto_amd.h declares,
+and rejects bad arguments without touching a GPU (CPU-only checks)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import lneto_amd as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lneto_amd.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lnx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ["lnx_crc32", "lnx_crc32_update", "lnx_crc32_search", "lnx_sum16_payload",
+              "lnx_crc32_batch", "lnx_fcs_verify_batch", "lnx_sum16_batch", "lnx_crc32_batch_multi"]:
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\sT\s+(lnx_\w+)", out))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    for s in declared_symbols():
+        assert getattr(L.lib, s) is not None
+
+
+def test_library_contains_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", L.LIB_PATH], capture_output=True, text=True)
+    assert ".hip_fatbin" in out.stdout
+    blob = open(L.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_batch_entry_points_validate_without_gpu():
+    # n == 0 is a no-op; NULL buffers with n > 0 are EINVAL (checked before any HIP call)
+    assert L.lib.lnx_crc32_batch(None, None, 0, None, None) == 0
+    assert L.lib.lnx_crc32_batch(None, None, 5, None, None) == L.LNX_EINVAL
+    assert L.lib.lnx_fcs_verify_batch(None, None, 5, None, None) == L.LNX_EINVAL
+    assert L.lib.lnx_sum16_batch(None, None, None, None, 5, None, None) == L.LNX_EINVAL
+    assert L.lib.lnx_crc32_batch_multi(0, None, None, None, None, None) == L.LNX_EINVAL
+    buf = (ctypes.c_uint8 * 8)()
+    off = (ctypes.c_uint64 * 2)(0, 100)  # offset beyond nbytes
+    out = (ctypes.c_uint32 * 1)()
+    assert L.lib.lnx_crc32_batch_host(ctypes.addressof(buf), 8, ctypes.addressof(off), 1,
+                                      ctypes.addressof(out), 0) == L.LNX_EINVAL
+
+
+def test_version_string():
+    assert "gfx950" in L.version()
+
+
+def test_cpp_host_api_compiles_and_runs(tmp_path):
+    """include/lneto_amd.hpp (C++ mirror of the Go API) against the built library."""
+    src = os.path.join(ROOT, "tests", "cpp", "test_host_api.cpp")
+    exe = tmp_path / "test_host_api"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), src,
+                    "-o", str(exe), "-L", os.path.dirname(L.LIB_PATH), "-llneto_amd",
+                    f"-Wl,-rpath,{os.path.dirname(L.LIB_PATH)}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
