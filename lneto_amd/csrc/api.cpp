@@ -14,6 +14,8 @@
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                bool verify, const void* image, int num_cus, hipStream_t stream);
+hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
+                                const void* image, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream);
@@ -23,16 +25,15 @@ std::vector<uint32_t> build_lds_image() {
   std::vector<uint32_t> img(kLdsDwords, 0);
   for (uint32_t m = 0; m < 4; ++m) {
     for (uint32_t e = 0; e < 256; ++e) {
-      const uint32_t v = zshift_bytes(e << (8 * m), kWindowBytes);  // U_m[e] = Z_256(e << 8m)
+      const uint32_t v = zshift_bytes(e << (8 * m), kStepBytes);  // U_m[e] = Z_64(e << 8m)
       for (uint32_t c = 0; c < 32; ++c) img[u_addr(m, e, c) / 4] = v;
     }
   }
-  for (uint32_t lane = 0; lane < 64; ++lane) {
-    for (uint32_t i = 0; i < 8; ++i) {
-      for (uint32_t v = 0; v < 16; ++v) {
-        img[f_addr(lane, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * (int64_t)lane);  // F_l = Z_{-4l}
-      }
-    }
+  for (uint32_t c = 0; c < 32; ++c) {
+    const int64_t p = c % kRowLanes;
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v)
+        img[f_addr(c, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * p);  // F_p = Z_{-4p}
   }
   return img;
 }
@@ -181,6 +182,20 @@ int lnx_crc32_batch_multi(int ngpu, const int* devices, const uint8_t* const* d_
   for (auto& t : th) t.join();
   for (int g = 0; g < ngpu; ++g)
     if (rcs[g] != LNX_OK) { g_last_error = errs[g]; return rcs[g]; }
+  return LNX_OK;
+}
+
+// Profiling hook (not in include/lneto_amd.h): kernel variants of DESIGN.md §4.
+int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
+                       void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_crc) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
   return LNX_OK;
 }
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Audit the CRC kernel's .s for hazards on the asm-loaded ring registers.
+
+The destination register of a streaming `global_load_dword ... nt` (issued
+by inline asm, invisible to hipcc's waitcnt pass) must not be read, copied or
+reused by any compiler-emitted instruction while that load may still be in
+flight: that would be a silent data race.  Checked in text order (which is the
+hot path's execution order): after each load its register is "outstanding"
+until a hand-written `s_waitcnt vmcnt(N)` retires it (all but the N youngest
+loads retire); any instruction naming an outstanding register is reported.
+usage: audit_ring.py file.s kernel-symbol
+"""
+import re
+import sys
+
+
+def regs(text):
+    out = set()
+    for t, a, b in re.findall(r"\b([vs])\[(\d+):(\d+)\]", text):
+        out |= {f"{t}{x}" for x in range(int(a), int(b) + 1)}
+    for t, a in re.findall(r"\b([vs])(\d+)\b", text):
+        out.add(f"{t}{a}")
+    return out
+
+
+def main():
+    path, sym = sys.argv[1], sys.argv[2]
+    lines = open(path).read().split("\n")
+    start = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
+    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    body = [l.split(";")[0].strip() for l in lines[start:end + 1]]
+    ring, first = set(), None
+    for i, t in enumerate(body):
+        if t.startswith("buffer_load_dword ") or (t.startswith("global_load_dword ") and t.endswith(" nt")):
+            ring |= regs(t.split(",")[0])
+            first = i if first is None else first
+    bad = []
+    # linear-order pending check: vmcnt(N) retires all but the N youngest loads
+    seq, pending = [], set()
+    for i, t in enumerate(body):
+        if t.startswith("s_waitcnt") and "vmcnt(" in t:
+            n = int(re.search(r"vmcnt\((\d+)\)", t).group(1))
+            seq = seq[-n:] if n else []
+            pending = {r for r in pending if r in seq}
+            continue
+        if t.startswith("buffer_load_dword ") or (t.startswith("global_load_dword ") and t.endswith(" nt")):
+            d = t.split(",")[0].split()[1]
+            pending.add(d)
+            seq.append(d)
+            continue
+        if not t or t.startswith("."):
+            continue
+        if regs(t.partition(" ")[2]) & pending:
+            bad.append((i, t, "touches a ring register whose load is outstanding"))
+    print(f"ring registers: {sorted(ring, key=lambda r: int(r[1:]))}")
+    for i, t, why in bad[:20]:
+        print(f"  {why}: {t}")
+    print(f"{len(bad)} hazards")
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
