@@ -65,6 +65,16 @@ __device__ __forceinline__ uint32_t u_step(const char* lds, uint32_t x, uint32_t
   return lds_rd(lds, a0) ^ lds_rd(lds, a1 + 128) ^ lds_rd(lds, a2) ^ lds_rd(lds, a3 + 128);
 }
 
+// U(x) ^ y with the four-way XOR in two v_bitop3 (gfx950 3-input logic op).
+__device__ __forceinline__ uint32_t u_step_xor(const char* lds, uint32_t x, uint32_t y, uint32_t b0, uint32_t b1) {
+  const uint32_t a0 = __builtin_amdgcn_perm(x, b0, 0x0c020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, b0, 0x0c020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, b1, 0x0c020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, b1, 0x0c020700u);
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(lds_rd(lds, a0), lds_rd(lds, a1 + 128), lds_rd(lds, a2), 0x96);
+  return __builtin_amdgcn_bitop3_b32(t, lds_rd(lds, a3 + 128), y, 0x96);
+}
+
 // F_p(r) through eight lane-private nibble tables.
 __device__ __forceinline__ uint32_t f_step(const char* lds, uint32_t r, uint32_t bf) {
   uint32_t acc = 0;
@@ -93,14 +103,54 @@ __device__ __forceinline__ uint32_t keep_from(int32_t lo) {
 
 __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
 
-// Streaming raw-buffer dword load; its completion is the caller's business
+// Streaming raw-buffer dword loads; their completion is the caller's business
 // (hipcc does not count asm loads, cdna_hip_programming.md §5.7 item 1): every
 // destination passes "+v" through the slot's vmcnt wait before its first use.
+// Each statement opens with s_nop 4: hipcc may restore the descriptor SGPRs
+// from a spill with v_readlane right before the statement, and a VALU SGPR
+// write needs 5 wait states before a VMEM instruction reads it as a
+// descriptor; hipcc pads that only for instructions it can see.
 template <int IMM>
 __device__ __forceinline__ uint32_t ld_buf(uint32_t voff, __amdgpu_buffer_rsrc_t rsrc) {
   uint32_t r;
-  asm volatile("buffer_load_dword %0, %1, %2, 0 offen offset:%3" : "=v"(r) : "v"(voff), "s"(rsrc), "i"(IMM));
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %1, %2, 0 offen offset:%3"
+               : "=v"(r) : "v"(voff), "s"(rsrc), "i"(IMM));
   return r;
+}
+// w[0] <- [v0], w[1] <- [v1]
+__device__ __forceinline__ void ld_buf2(uint32_t& a, uint32_t& b, uint32_t v0, uint32_t v1,
+                                        __amdgpu_buffer_rsrc_t rsrc) {
+  asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %4, 0 offen\n\tbuffer_load_dword %1, %3, %4, 0 offen"
+               : "=v"(a), "=v"(b) : "v"(v0), "v"(v1), "s"(rsrc));
+}
+// N loads from one VGPR offset at immediates IMM0, IMM0+64, ...
+template <int IMM0, int N>
+__device__ __forceinline__ void ld_run(uint32_t* o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
+  constexpr int D = (int)kStepBytes;
+  if constexpr (N == 6) {
+    asm volatile("s_nop 4\n\t"
+                 "buffer_load_dword %0, %6, %7, 0 offen offset:%8\n\t"
+                 "buffer_load_dword %1, %6, %7, 0 offen offset:%9\n\t"
+                 "buffer_load_dword %2, %6, %7, 0 offen offset:%10\n\t"
+                 "buffer_load_dword %3, %6, %7, 0 offen offset:%11\n\t"
+                 "buffer_load_dword %4, %6, %7, 0 offen offset:%12\n\t"
+                 "buffer_load_dword %5, %6, %7, 0 offen offset:%13"
+                 : "=v"(o[0]), "=v"(o[1]), "=v"(o[2]), "=v"(o[3]), "=v"(o[4]), "=v"(o[5])
+                 : "v"(v), "s"(rsrc), "i"(IMM0), "i"(IMM0 + D), "i"(IMM0 + 2 * D), "i"(IMM0 + 3 * D),
+                   "i"(IMM0 + 4 * D), "i"(IMM0 + 5 * D));
+  } else if constexpr (N == 5) {
+    asm volatile("s_nop 4\n\t"
+                 "buffer_load_dword %0, %5, %6, 0 offen offset:%7\n\t"
+                 "buffer_load_dword %1, %5, %6, 0 offen offset:%8\n\t"
+                 "buffer_load_dword %2, %5, %6, 0 offen offset:%9\n\t"
+                 "buffer_load_dword %3, %5, %6, 0 offen offset:%10\n\t"
+                 "buffer_load_dword %4, %5, %6, 0 offen offset:%11"
+                 : "=v"(o[0]), "=v"(o[1]), "=v"(o[2]), "=v"(o[3]), "=v"(o[4])
+                 : "v"(v), "s"(rsrc), "i"(IMM0), "i"(IMM0 + D), "i"(IMM0 + 2 * D), "i"(IMM0 + 3 * D),
+                   "i"(IMM0 + 4 * D));
+  } else {
+    static_assert(N == 5 || N == 6, "run length");
+  }
 }
 
 // vmcnt wait naming every register of one slot.
@@ -114,13 +164,19 @@ __device__ __forceinline__ void slot_wait(uint32_t (&w)[W], uint32_t& bnd) {
                    "+v"(w[20]), "+v"(w[21]), "+v"(w[22]), "+v"(w[23]), "+v"(w[24])
                  : "i"(N));
     asm volatile("" : "+v"(bnd));
+  } else if constexpr (W == 13) {
+    asm volatile("s_waitcnt vmcnt(%13)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                   "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12])
+                 : "i"(N));
+    asm volatile("" : "+v"(bnd));
   } else if constexpr (W == 7) {
     asm volatile("s_waitcnt vmcnt(%7)"
                  : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6])
                  : "i"(N));
     asm volatile("" : "+v"(bnd));
   } else {
-    static_assert(W == 25 || W == 7, "unsupported item size");
+    static_assert(W == 25 || W == 13 || W == 7, "unsupported item size");
   }
 }
 
@@ -183,7 +239,7 @@ __device__ __forceinline__ void rows_body(const WaveCtx& cx) {
   static_assert(S >= 2 && 4 * S + 1 <= 64, "ring size");
   static_assert(KS * (int)kStepBytes <= 4095, "buffer immediate offset");
   constexpr int kW = KS + 1;                    // w[0] = the step before the item
-  constexpr int kPending = (S - 1) * (KS + 2);  // loads issued after a slot's own
+  constexpr int kPending = (S - 1) * (VAR == 2 ? 1 : KS + 2);  // loads issued after a slot's own
   const char* lds = cx.lds;
   const uint32_t lane = cx.lane, p = cx.p, row = cx.row, bu0 = cx.bu0, bu1 = cx.bu1, bf = cx.bf;
   const uint32_t nwf = cx.nwf, o0_lo = cx.o0_lo, adj = cx.adj;
@@ -281,11 +337,19 @@ __device__ __forceinline__ void rows_body(const WaveCtx& cx) {
 #pragma unroll
       for (int k = 0; k < kW; ++k) w[s][k] = voff * 0x9E3779B1u + k;
     } else {
-      w[s][0] = ld_buf<0>(v0, data_rsrc);
-      w[s][1] = ld_buf<0>(v1, data_rsrc);
-      [&]<int... K>(std::integer_sequence<int, K...>) {
-        ((w[s][K + 2] = ld_buf<K * (int)kStepBytes>(v2, data_rsrc)), ...);
-      }(std::make_integer_sequence<int, kW - 2>{});
+      ld_buf2(w[s][0], w[s][1], v0, v1, data_rsrc);
+      if constexpr (KS == 24) {  // w[2..24]: 6 + 6 + 6 + 5
+        ld_run<0, 6>(&w[s][2], v2, data_rsrc);
+        ld_run<6 * (int)kStepBytes, 6>(&w[s][8], v2, data_rsrc);
+        ld_run<12 * (int)kStepBytes, 6>(&w[s][14], v2, data_rsrc);
+        ld_run<18 * (int)kStepBytes, 5>(&w[s][20], v2, data_rsrc);
+      } else if constexpr (KS == 12) {  // w[2..12]: 6 + 5
+        ld_run<0, 6>(&w[s][2], v2, data_rsrc);
+        ld_run<6 * (int)kStepBytes, 5>(&w[s][8], v2, data_rsrc);
+      } else {
+        static_assert(KS == 6, "load runs are written out for KS = 6, 12 and 24");
+        ld_run<0, 5>(&w[s][2], v2, data_rsrc);
+      }
     }
     // 4. bounds of the next 4S+1 frames, for this slot's next issue
     nfb[s] = nf;
@@ -330,19 +394,22 @@ __device__ __forceinline__ void rows_body(const WaveCtx& cx) {
       for (int k = 0; k < KS; ++k) reg ^= w[s][k + 1];
     } else {
       if (full && !unaligned) {
-        // hot path: every row folds KS steps of a 4-byte-aligned frame, no predication
+        // hot path: every row folds KS steps of a 4-byte-aligned frame, no
+        // predication; the next word is XOR-ed in by the step's second bitop3
+        uint32_t in = reg ^ word(0, false);
 #pragma unroll
-        for (int k = 0; k < KS; ++k) reg = u_step(lds, reg ^ word(k, false), bu0, bu1);
+        for (int k = 0; k < KS - 1; ++k) in = u_step_xor(lds, in, word(k + 1, false), bu0, bu1);
+        reg = u_step_xor(lds, in, 0u, bu0, bu1);
       } else if (!unaligned) {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-          const uint32_t r2 = u_step(lds, reg ^ word(k, false), bu0, bu1);
+          const uint32_t r2 = u_step_xor(lds, reg ^ word(k, false), 0u, bu0, bu1);
           reg = (uint32_t)k < ns ? r2 : reg;
         }
       } else {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
-          const uint32_t r2 = u_step(lds, reg ^ word(k, true), bu0, bu1);
+          const uint32_t r2 = u_step_xor(lds, reg ^ word(k, true), 0u, bu0, bu1);
           reg = (uint32_t)k < ns ? r2 : reg;
         }
       }
@@ -392,9 +459,9 @@ __device__ __forceinline__ void rows_body(const WaveCtx& cx) {
 
 // ------------------------------------------------------------------ kernel
 // Item size per wave: long frames use 24-step items (a 1500-byte frame is one
-// item, 2 slots in flight), short frames 6-step items with 4 slots, so rows
+// item, 2 slots), short frames 6-step items with 4 slots, so rows
 // idle less at frame ends.  Chosen per wave from its mean frame length.
-template <CrcMode MODE, int VAR = 0>
+template <CrcMode MODE, int VAR = 0, int KSL = 24, int SL = 2>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ image, void* __restrict__ out) {
@@ -456,7 +523,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   cx.off_rsrc = off_rsrc;
   cx.out_rsrc = out_rsrc;
   if (range >= (uint64_t)nwf * 768u)
-    rows_body<MODE, 24, 2, VAR>(cx);
+    rows_body<MODE, KSL, SL, VAR>(cx);
   else
     rows_body<MODE, 6, 4, VAR>(cx);
 }
@@ -471,19 +538,23 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const uint64_t fpw = (n + waves - 1) / waves;
   const uint4* img = static_cast<const uint4*>(image);
   const dim3 g((unsigned)grid), b(kBlockThreads);
+#define LNX_LAUNCH(M, V, K, S) \
+  hipLaunchKernelGGL((crc32_rows_kernel<M, V, K, S>), g, b, 0, stream, bytes, off, n, fpw, img, out)
   if (verify) {
-    hipLaunchKernelGGL((crc32_rows_kernel<CrcMode::kVerify, 0>), g, b, 0, stream, bytes, off,
-                       n, fpw, img, out);
-  } else if (var == 1) {
-    hipLaunchKernelGGL((crc32_rows_kernel<CrcMode::kCrc, 1>), g, b, 0, stream, bytes, off, n,
-                       fpw, img, out);
-  } else if (var == 2) {
-    hipLaunchKernelGGL((crc32_rows_kernel<CrcMode::kCrc, 2>), g, b, 0, stream, bytes, off, n,
-                       fpw, img, out);
+    LNX_LAUNCH(CrcMode::kVerify, 0, 24, 2);
   } else {
-    hipLaunchKernelGGL((crc32_rows_kernel<CrcMode::kCrc, 0>), g, b, 0, stream, bytes, off, n,
-                       fpw, img, out);
+    switch (var) {
+      case 1: LNX_LAUNCH(CrcMode::kCrc, 1, 24, 2); break;
+      case 2: LNX_LAUNCH(CrcMode::kCrc, 2, 24, 2); break;
+      case 10: LNX_LAUNCH(CrcMode::kCrc, 0, 24, 3); break;
+      case 11: LNX_LAUNCH(CrcMode::kCrc, 0, 12, 3); break;
+      case 12: LNX_LAUNCH(CrcMode::kCrc, 0, 12, 4); break;
+      case 13: LNX_LAUNCH(CrcMode::kCrc, 1, 24, 3); break;
+      case 14: LNX_LAUNCH(CrcMode::kCrc, 1, 12, 4); break;
+      default: LNX_LAUNCH(CrcMode::kCrc, 0, 24, 2); break;
+    }
   }
+#undef LNX_LAUNCH
   return hipGetLastError();
 }
 

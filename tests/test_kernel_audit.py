@@ -1,0 +1,33 @@
+"""Static audit of the compiled CRC kernels (CPU only; needs hipcc, no GPU).
+
+The streaming loads are inline asm that hipcc neither counts for vmcnt nor pads
+for hazards, so two classes of bug compile silently and surface only as wrong
+CRCs or GPU memory faults on the box.  tools/prof/audit_ring.py checks every
+instantiation's .s for (1) a compiler instruction touching a ring register
+while its load is outstanding and (2) a VALU write of a buffer-descriptor SGPR
+fewer than 5 wait states before an asm buffer load that reads it.
+"""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "lneto_amd", "csrc", "crc32_kernel.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path):
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-c", "--save-temps",
+                    "-o", str(tmp_path / "k.o"), SRC], cwd=tmp_path, check=True, capture_output=True)
+    asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
+    text = open(tmp_path / asm).read()
+    syms = re.findall(r"^(_ZN3lnx17crc32_rows_kernel\w+):", text, flags=re.M)
+    assert len(syms) >= 3
+    for sym in syms:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_ring.py"),
+                            str(tmp_path / asm), sym], capture_output=True, text=True)
+        assert r.returncode == 0, f"{sym}:\n{r.stdout}"

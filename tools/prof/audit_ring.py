@@ -52,6 +52,30 @@ def main():
             continue
         if regs(t.partition(" ")[2]) & pending:
             bad.append((i, t, "touches a ring register whose load is outstanding"))
+    # descriptor hazard: a VALU write of an SGPR (v_readlane, v_readfirstlane,
+    # v_cmp with SGPR dst, ...) needs 5 wait states before a VMEM reads it as a
+    # descriptor; hipcc pads only instructions it can see, so every asm buffer
+    # load must be preceded by an s_nop >= 4 (or >= 5 other instructions).
+    for i, t in enumerate(body):
+        if not t.startswith("buffer_load_dword "):
+            continue
+        rs = regs(t.split(",")[2]) if len(t.split(",")) > 2 else set()
+        waits = 0
+        for j in range(i - 1, max(i - 8, -1), -1):
+            u = body[j]
+            if not u or u.startswith("."):
+                continue
+            if u.startswith("s_nop"):
+                waits += int(u.split()[1]) + 1
+            elif u.startswith("v_"):
+                dst = u.partition(" ")[2].split(",")[0]
+                if regs(dst) & rs and waits < 5:
+                    bad.append((i, t, f"descriptor written by VALU {waits} wait states before: {u}"))
+                waits += 1
+            else:
+                waits += 1
+            if waits >= 5:
+                break
     print(f"ring registers: {sorted(ring, key=lambda r: int(r[1:]))}")
     for i, t, why in bad[:20]:
         print(f"  {why}: {t}")

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise a tools/prof/profile.sh run into profiles/ (committed evidence).
+
+usage: summarize.py gpurun_out/prof_TAG_WL  profiles/  TAG  WL
+Writes  profiles/TAG_WL_kernel_stats.csv   (rocprofv3 --stats, verbatim)
+        profiles/TAG_WL_summary.json       (per-launch averages of every counter)
+        profiles/traffic_WL.json           (HBM bytes per launch, calibrated; read by bench.py)
+"""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "crc32_rows_kernel"
+CAL_BYTES = 2 << 30
+
+
+def per_dispatch(path, match):
+    rows = list(csv.DictReader(open(path)))
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in rows:
+        if match in r["Kernel_Name"]:
+            acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    src, dst, tag, wl = sys.argv[1:5]
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "trace_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_{wl}_kernel_stats.csv"))
+    kern = [r for r in csv.DictReader(open(stats)) if KERNEL in r["Name"]]
+    summary = {"workload": wl, "kernel": kern[0]["Name"] if kern else None,
+               "avg_ns": float(kern[0]["AverageNs"]) if kern else None,
+               "calls": int(kern[0]["Calls"]) if kern else None, "counters": {}}
+    for i in range(1, 10):
+        p = os.path.join(src, f"pmc{i}", "pmc_counter_collection.csv")
+        if os.path.exists(p):
+            avg, n = per_dispatch(p, KERNEL)
+            summary["counters"].update(avg)
+    cal, _ = per_dispatch(os.path.join(src, "calib", "calib_counter_collection.csv"), "rd<unsigned int>")
+    cal4, _ = per_dispatch(os.path.join(src, "calib", "calib_counter_collection.csv"), "rd<HIP_vector_type")
+    # FETCH_SIZE is in KiB; bytes actually fetched per KiB-unit for this access width:
+    f_dw = CAL_BYTES / (cal["FETCH_SIZE"] * 1024) if cal else None
+    f_x4 = CAL_BYTES / (cal4["FETCH_SIZE"] * 1024) if cal4 else None
+    summary["calibration"] = {"bytes_per_fetch_size_byte_dword_loads": f_dw,
+                              "bytes_per_fetch_size_byte_dwordx4_loads": f_x4,
+                              "calib_bytes": CAL_BYTES}
+    fs = summary["counters"].get("FETCH_SIZE")
+    if fs and f_dw:
+        hbm = fs * 1024 * f_dw
+        summary["hbm_bytes_per_launch"] = hbm
+        with open(os.path.join(dst, f"traffic_{wl}.json"), "w") as fh:
+            json.dump({"hbm_bytes_per_launch": round(hbm), "fetch_size_kib": fs,
+                       "calibration_factor": f_dw, "source": f"{tag}_{wl}_summary.json",
+                       "method": "rocprofv3 --pmc FETCH_SIZE, own pass; x factor measured on tools/prof/calib "
+                                 "(dword-per-lane reads of 2 GiB) in the same profiling run"}, fh, indent=1)
+    c = summary["counters"]
+    if "GRBM_GUI_ACTIVE" in c and summary["avg_ns"]:
+        summary["clock_ghz_est"] = c["GRBM_GUI_ACTIVE"] / 8 / summary["avg_ns"]
+    with open(os.path.join(dst, f"{tag}_{wl}_summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -20,7 +20,8 @@ d = synth.bytes_torch(int(off[-1]), dev)
 o = torch.from_numpy(off.astype(np.int64)).to(dev)
 out = torch.empty(n, dtype=torch.int32, device=dev)
 s = torch.cuda.current_stream()
-for var in (0, 1, 2, 0):
+vars_ = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2, 0]
+for var in vars_:
     for _ in range(3):
         L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream)
     torch.cuda.synchronize()

@@ -1,0 +1,71 @@
+// Read-bandwidth ceiling of the CRC kernel's access patterns (no compute):
+// a wave = 4 rows; each row streams its own contiguous "frame" of FB bytes,
+// W bytes per lane per load (row covers 16*W bytes per load instruction).
+// Frames are packed back to back; each wave owns a contiguous range of frames.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+
+template <int W> struct V;
+template <> struct V<4> { typedef uint32_t T; };
+template <> struct V<8> { typedef uint2 T; };
+template <> struct V<16> { typedef uint4 T; };
+__device__ inline uint32_t fold(uint32_t v) { return v; }
+__device__ inline uint32_t fold(uint2 v) { return v.x ^ v.y; }
+__device__ inline uint32_t fold(uint4 v) { return v.x ^ v.y ^ v.z ^ v.w; }
+
+template <int W, int ROWS, int U>
+__global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, uint64_t nframes, uint32_t fb,
+                                            uint64_t fpw, uint32_t* out) {
+  typedef typename V<W>::T T;
+  __shared__ uint32_t pad[40960];
+  const uint32_t lane = threadIdx.x & 63, rl = 64 / ROWS, p = lane % rl, row = lane / rl;
+  const uint64_t gw = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint64_t f0 = gw * fpw, f1 = std::min<uint64_t>(f0 + fpw, nframes);
+  uint32_t acc = 0;
+  const uint32_t rowbytes = rl * W;
+  for (uint64_t f = f0 + row; f < f1; f += ROWS) {
+    const uint8_t* fr = base + f * fb;
+    for (uint32_t o = 0; o < fb; o += rowbytes * U) {
+      T v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t oo = o + u * rowbytes + p * W;
+        v[u] = oo + W <= fb ? *(const T*)(fr + oo) : T{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc ^= fold(v[u]);
+    }
+  }
+  pad[threadIdx.x] = acc;
+  __syncthreads();
+  if (pad[(threadIdx.x + 1) & 1023] == 0x12345678u) out[0] = acc;
+}
+
+template <typename F>
+float tm(F fn) {
+  hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  fn(); (void)hipDeviceSynchronize();
+  std::vector<float> t;
+  for (int r = 0; r < 7; ++r) { (void)hipEventRecord(a); fn(); (void)hipEventRecord(b); (void)hipEventSynchronize(b);
+    float ms; (void)hipEventElapsedTime(&ms, a, b); t.push_back(ms); }
+  std::sort(t.begin(), t.end()); return t[3];
+}
+
+int main() {
+  const uint32_t fb = 1536;  // frame bytes (multiple of 256 so every pattern tiles it)
+  const uint64_t nframes = 1 << 20;
+  uint8_t* buf; uint32_t* out;
+  (void)hipMalloc(&buf, nframes * fb); (void)hipMalloc(&out, 64);
+  (void)hipMemset(buf, 3, nframes * fb);
+  const uint64_t waves = 256 * 16, fpw = (nframes + waves - 1) / waves;
+#define RUN(W, R, U) { float ms = tm([&] { pat<W, R, U><<<256, 1024>>>(buf, nframes, fb, fpw, out); }); \
+  printf("W=%2d rows=%d unroll=%d rowbytes/load=%4d : %.3f ms %.1f GB/s\n", W, R, U, 64 / R * W, ms, nframes * fb / ms / 1e6); }
+  RUN(4, 4, 6); RUN(4, 4, 12); RUN(4, 4, 24);
+  RUN(8, 4, 6); RUN(8, 4, 12);
+  RUN(16, 4, 3); RUN(16, 4, 6);
+  RUN(4, 1, 6); RUN(16, 1, 1); RUN(16, 2, 3);
+  return 0;
+}
