@@ -203,7 +203,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "lnx::crc32_frames_kernel<kCrc>",
+            "kernel": "lnx::crc32_rows_kernel<kCrc>",
             "kernel_ms": round(kern_ms, 4),
             "algorithmic_bytes_per_launch": nbytes,
         },

@@ -208,7 +208,7 @@ int lnx_device_count(void) {
 const char* lnx_last_error(void) { return g_last_error.c_str(); }
 
 const char* lnx_version(void) {
-  return "lneto_amd 0.1 gfx950: crc32 wave-per-frame/lane-private-LDS-U256 + sum16 wave-per-segment";
+  return "lneto_amd 0.2 gfx950: crc32 rows (4 frames/wave, lane-private LDS U=Z_64, buffer-load ring) + sum16 wave-per-segment";
 }
 
 }  // extern "C"
