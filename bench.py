@@ -5,7 +5,11 @@ Metric (BASELINE.json): GiB/s of CRC-32 over device-resident 1500-byte frames,
 with the fraction of the HBM3E read roofline.  One "step" = one
 lnx_crc32_batch call over the rank's whole frame batch (inputs already in HBM).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--op OP]
+
+--op crc32 (default, the BASELINE metric) | fcs_verify (lnx_fcs_verify_batch,
+residue check of the same frames) | sum16 (lnx_sum16_batch: RFC 791 checksum of
+every frame as one segment, random pseudo-header seeds).
 
 N=1 runs BASELINE configs[1] (1 M x 1500 B).  For N>1 (launched by
 torch.distributed.run, one rank per GPU) every rank owns its own contiguous
@@ -58,22 +62,33 @@ def workload_spec(name: str, world: int):
     raise SystemExit(f"unknown workload {name}")
 
 
-def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: int | None = None):
+def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: int | None = None, op: str = "crc32"):
     """Time the C oracle (restatement of Go hash/crc32 slicing-by-8 as called by
-    ethernet/crc.go:19-21) on a bounded sample of the same frames."""
+    ethernet/crc.go:19-21; for --op sum16 the crc.go:52-59 restatement) on a
+    bounded sample of the same frames."""
     from oracle import oracle as O
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
+    if op == "sum16":
+        threads = 1  # the C oracle's segment sum is single-threaded
     nsamp = min(len(off_np) - 1, 1 << 16)
     sample_bytes = int(off_np[nsamp] - off_np[0])
     host = d_bytes[int(off_np[0]):int(off_np[nsamp])].cpu().numpy()
     off_s = (off_np[:nsamp + 1] - off_np[0]).astype(np.uint64)
     res = {}
+    lens_s = np.diff(off_s).astype(np.uint32)
+
+    def run(t):
+        if op == "sum16":
+            O.sum16_segments(host, off_s[:-1], lens_s, None)
+        else:
+            O.crc32_frames(host, off_s, threads=t)
+
     for t in sorted({1, threads}):
-        O.crc32_frames(host, off_s, threads=t)  # warm
+        run(t)  # warm
         reps, t0 = 0, time.perf_counter()
         while True:
-            O.crc32_frames(host, off_s, threads=t)
+            run(t)
             reps += 1
             el = time.perf_counter() - t0
             if el >= budget_s / 2:
@@ -83,8 +98,10 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
         "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "value_1core": round(res[1], 3),
         "sample": f"{nsamp} frames x {frame_len or 'zipf'} B ({sample_bytes/1e6:.0f} MB) of the same synthetic batch, "
-                  f"repeated for ~{budget_s/2:.0f}s per thread count; C restatement of Go hash/crc32 "
-                  f"(slicing-by-8), NOT lneto's Go binary (no Go toolchain on the box)",
+                  f"repeated for ~{budget_s/2:.0f}s per thread count; " + (
+                      "C restatement of lneto crc.go PayloadSum16" if op == "sum16" else
+                      "C restatement of Go hash/crc32 (slicing-by-8)") +
+                  ", NOT lneto's Go binary (no Go toolchain on the box)",
     }
 
 
@@ -95,6 +112,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
+    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
@@ -134,10 +152,22 @@ def main():
     d_off = torch.from_numpy(off_np.astype(np.int64)).to(dev)
     d_crc = torch.empty(n_local, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    if args.op == "sum16":
+        d_seg = d_off[:-1].contiguous()
+        d_len = (d_off[1:] - d_off[:-1]).to(torch.int32)
+        d_seed = torch.randint(0, 1 << 20, (n_local,), dtype=torch.int32, device=dev)
+        d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
+    elif args.op == "fcs_verify":
+        d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
 
     def step():
-        L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
+        if args.op == "sum16":
+            L.sum16_batch(d_bytes, d_seg, d_len, d_seed, out=d_sum, stream=stream)
+        elif args.op == "fcs_verify":
+            L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+        else:
+            L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -173,8 +203,13 @@ def main():
     value = total_bytes * args.steps / elapsed_max / 2**30
     achieved = nbytes / (kern_ms * 1e-3) / 1e9  # GB/s, this rank's launches, HIP-event timed
 
+    metric = {
+        "crc32": "GiB/s CRC-32 over device-resident 1500B frames; % of HBM3E read peak",
+        "fcs_verify": "GiB/s FCS verify (CRC-32 residue) over device-resident frames; % of HBM3E read peak",
+        "sum16": "GiB/s RFC 791 internet checksum over device-resident segments; % of HBM3E read peak",
+    }[args.op]
     out = {
-        "metric": "GiB/s CRC-32 over device-resident 1500B frames; % of HBM3E read peak",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -203,12 +238,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "lnx::crc32_rows_kernel<kCrc>",
+            "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
+                       "sum16": "lnx::sum16_segments_kernel"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "algorithmic_bytes_per_launch": nbytes,
         },
     }
-    traffic_file = os.path.join(ROOT, "profiles", f"traffic_{wname}.json")
+    tag = wname if args.op == "crc32" else f"{wname}_{args.op}"
+    traffic_file = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(traffic_file):
         with open(traffic_file) as fh:
             tr = json.load(fh)
@@ -218,10 +255,23 @@ def main():
     if args.verify:
         from oracle import oracle as O
         idx = np.random.default_rng(rank).choice(n_local, min(256, n_local), replace=False)
-        got = d_crc.cpu().numpy().view(np.uint32)
+        if args.op == "sum16":
+            got = d_sum.cpu().numpy().view(np.uint16)
+            seeds = d_seed.cpu().numpy().view(np.uint32)
+        elif args.op == "fcs_verify":
+            got = d_ok.cpu().numpy()
+        else:
+            got = d_crc.cpu().numpy().view(np.uint32)
         for i in idx:
             s, e = int(off_np[i]), int(off_np[i + 1])
-            assert int(got[i]) == O.crc32(d_bytes[s:e].cpu().numpy().tobytes()), f"mismatch frame {i}"
+            fr = d_bytes[s:e].cpu().numpy().tobytes()
+            if args.op == "sum16":
+                want = O.payload_sum16(int(seeds[i]), fr)
+            elif args.op == "fcs_verify":
+                want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
+            else:
+                want = O.crc32(fr)
+            assert int(got[i]) == want, f"mismatch frame {i}"
         out["verified_sample"] = len(idx)
 
     if args.with_copies and rank == 0:
@@ -242,7 +292,7 @@ def main():
                                  "note": "pinned H2D of frames + kernel + D2H of CRCs, serial, 1 stream"}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget, op=args.op)
 
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -105,6 +105,22 @@ int lnx_fcs_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t
 int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
                     const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream);
 
+/* Receive-path checksum verdicts, one fused kernel: for
+ * every Ethernet frame d_bytes[d_off[i] : d_off[i+1]] (FCS already stripped)
+ * d_verdict[i] = the result lneto's receive path reaches at its checksum
+ * stage — StackEthernet.Demux size checks (internet/stack-ethernet.go:139-165),
+ * then by EtherType demux4 (internet/stack-ip4.go:100-164: ValidateExceptCRC,
+ * IPv4 header sum over the first 20 bytes, TCP / UDP sums with pseudo-header)
+ * or demux6 (internet/stack-ip6.go:86-138).  0 = all checks passed or none
+ * applies (other EtherTypes); otherwise the lneto errGeneric value
+ * (errors.go:6-28): 2 ErrPacketDrop (evil bit, only with LNX_VERIFY_EVIL_BIT),
+ * 3 ErrBadCRC, 14 ErrInvalidField, 15 ErrInvalidLengthField,
+ * 18 ErrTruncatedFrame.  Destination filtering and handler lookup are stack
+ * configuration and are taken as accept-all. */
+#define LNX_VERIFY_EVIL_BIT 1u /* lneto.ValidateEvilBit on the stack's Validator */
+int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                             uint8_t* d_verdict, void* stream);
+
 /* Host-memory convenience: copies h_bytes/h_off to the device, runs
  * lnx_crc32_batch, copies the CRCs back, synchronously.  Used to measure the
  * PCIe-inclusive rate.  nbytes is the length of h_bytes; every

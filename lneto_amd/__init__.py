@@ -25,7 +25,8 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblneto_amd.so")
+# LNETO_AMD_LIB selects an alternative in-tree build (profiling experiments only).
+LIB_PATH = os.environ.get("LNETO_AMD_LIB") or os.path.join(HERE, "liblneto_amd.so")
 CRC32_RESIDUE = 0x2144DF1C
 
 LNX_OK, LNX_EINVAL, LNX_ENODEV, LNX_EHIP, LNX_ENOMEM = 0, -1, -2, -3, -5
@@ -66,6 +67,7 @@ _sig = {
     "lnx_crc32_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_fcs_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_sum16_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_ingress_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
     "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
@@ -197,6 +199,23 @@ def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
     if n > 0:
         _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
                                         _stream_ptr(stream)), "lnx_fcs_verify_batch")
+    return out
+
+
+VERIFY_EVIL_BIT = 1  # LNX_VERIFY_EVIL_BIT
+
+
+def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None):
+    """Receive-path checksum verdict per Ethernet frame (lnx_ingress_verify_batch):
+    0 = checks passed / none apply, else lneto's errGeneric code (3 = ErrBadCRC, ...)."""
+    import torch
+    _dev_check(d_bytes, d_off)
+    n = d_off.numel() - 1
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.uint8, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_ingress_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags, out.data_ptr(),
+                                            _stream_ptr(stream)), "lnx_ingress_verify_batch")
     return out
 
 

@@ -16,24 +16,32 @@ hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64
                                bool verify, const void* image, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* image, int num_cus, hipStream_t stream);
+hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
+                                 uint8_t* verdict, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream);
 
-// The 160 KiB LDS image (lds_layout.hpp), built once on the host.
-std::vector<uint32_t> build_lds_image() {
+// The 160 KiB LDS image of row width rl (lds_layout.hpp), built once on the host.
+std::vector<uint32_t> build_lds_image(uint32_t rl) {
   std::vector<uint32_t> img(kLdsDwords, 0);
+  const int64_t sb = 4 * (int64_t)rl;
   for (uint32_t m = 0; m < 4; ++m) {
     for (uint32_t e = 0; e < 256; ++e) {
-      const uint32_t v = zshift_bytes(e << (8 * m), kStepBytes);  // U_m[e] = Z_64(e << 8m)
+      const uint32_t v = zshift_bytes(e << (8 * m), sb);  // U_m[e] = Z_SB(e << 8m)
       for (uint32_t c = 0; c < 32; ++c) img[u_addr(m, e, c) / 4] = v;
     }
   }
   for (uint32_t c = 0; c < 32; ++c) {
-    const int64_t p = c % kRowLanes;
+    const int64_t p = c % rl;
     for (uint32_t i = 0; i < 8; ++i)
       for (uint32_t v = 0; v < 16; ++v)
         img[f_addr(c, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * p);  // F_p = Z_{-4p}
+    const uint32_t q0 = (uint32_t)p & 7u;
+    for (uint32_t h = 0; h < 2; ++h)
+      for (uint32_t t = 0; t < 4; ++t)
+        for (uint32_t v = 0; v < 16; ++v)
+          img[t_addr(c, h, t, v) / 4] = zshift_bytes(v << (4 * (q0 + 4 * h)), -(int64_t)t);  // Z_{-t}
   }
   return img;
 }
@@ -57,8 +65,14 @@ struct DeviceCtx {
 constexpr int kMaxDevices = 64;
 DeviceCtx g_ctx[kMaxDevices];
 
+// Both images back to back: [RL = 16][RL = 4] (lds_layout.hpp image_index).
 const std::vector<uint32_t>& host_image() {
-  static const std::vector<uint32_t> img = build_lds_image();
+  static const std::vector<uint32_t> img = [] {
+    std::vector<uint32_t> all = build_lds_image(16);
+    const std::vector<uint32_t> i4 = build_lds_image(4);
+    all.insert(all.end(), i4.begin(), i4.end());
+    return all;
+  }();
   return img;
 }
 
@@ -123,6 +137,19 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
   hipError_t e = launch_sum16_segments(d_bytes, d_off, d_len, d_seed, n, d_out, c->num_cus,
                                        static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "sum16_segments_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                             uint8_t* d_verdict, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_verdict) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags, d_verdict, c->num_cus,
+                                       static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "ingress_verify_kernel launch");
   return LNX_OK;
 }
 

@@ -1,8 +1,11 @@
-// lds_layout.hpp — geometry of the CRC-32 kernel and byte layout of its LDS image.
+// lds_layout.hpp — geometry of the CRC-32 kernel and byte layout of its LDS images.
 //
-// Geometry: a wave is four 16-lane "rows"; each row folds one frame.  Lane p of
-// a row (p = lane % 16) consumes the 4-byte word at window offset 4p + 64j, so
-// a row advances 64 bytes per step and a wave 256 bytes per dword load.
+// Geometry: a wave is 64/RL "rows" of RL lanes; each row folds one frame.  Lane
+// p of a row (p = lane % RL) consumes the 4-byte word at window offset
+// 4p + SB*j, SB = 4*RL, so a row advances SB bytes per step.  Two row widths
+// exist: RL = 16 (4 frames per wave, 64-byte steps) for long
+// frames and RL = 4 (16 frames per wave, 16-byte steps) for short ones.  Each
+// has its own 160 KiB image; a workgroup loads the one its frames call for.
 //
 // One 1024-thread workgroup per CU holds the image.  Every table is
 // "lane-private": lane l only ever reads LDS bank (l % 32), so a ds_read_b32
@@ -10,28 +13,35 @@
 // index is.  Measured on MI355X: ~21-24 lookups/clk/CU this way vs ~9.9 for a
 // shared table with random indices.
 //
-// U region [0, 128 KiB): the row stride map U = Z_64 (advance the CRC register
-// over 64 bytes) as four byte tables U_m[e] = Z_64(e << 8m):
+// U region [0, 128 KiB): the row stride map U = Z_SB (advance the CRC register
+// over SB bytes) as four byte tables U_m[e] = Z_SB(e << 8m):
 //     byte address = (m>>1)<<16 | e<<8 | (m&1)<<7 | c<<2        (c = lane%32)
 // so the address of U_m[byte k of x] is v_perm(x, base_m, sel_k) — one VALU op:
 // byte 1 of the address is the data byte, bytes 0 and 2 come from a per-lane
 // base; m&1 is folded into the ds_read immediate offset (+128).
 //
 // F region [128 KiB, 144 KiB): per-lane final alignment F_p = Z_{-4p} (lane p's
-// register ends 4p bytes past the frame end) as eight 16-entry nibble tables:
+// register ends 4p bytes past the window end) as eight 16-entry nibble tables:
 //     byte address = 128K | i<<11 | v<<7 | c<<2          (nibble i, value v)
-// F_p(r) = XOR_i F_p,i[(r >> 4i) & 15]; column c holds the tables of p = c%16,
-// which serves lanes c and c+32 alike.  [144 KiB, 160 KiB) is unused.
+// F_p(r) = XOR_i F_p,i[(r >> 4i) & 15]; column c holds the tables of
+// p = c % RL, which serves lanes c and c+32 alike.
+//
+// T region [144 KiB, 160 KiB): the window ends at the frame end rounded up to
+// 4 bytes, t = 0..3 bytes past it, so the row's register needs Z_{-t} too.  The
+// row's lanes share that work by nibble: entry (h, t, v) of column c is
+// Z_{-t}(v << 4q_h) with q_0 = (c % RL) & 7 and q_1 = q_0 + 4 (h = 1 is used
+// by RL = 4 only, where each lane covers two nibbles):
+//     byte address = 144K | (64h + 16t + v)<<7 | c<<2
 #pragma once
 #include <cstdint>
 
 namespace lnx {
 
-constexpr uint32_t kRowLanes = 16;                 // lanes folding one frame
-constexpr uint32_t kStepBytes = kRowLanes * 4;     // bytes a row consumes per step
 constexpr uint32_t kLdsBytes = 163840;             // 160 KiB (whole CU)
 constexpr uint32_t kLdsDwords = kLdsBytes / 4;
 constexpr uint32_t kFBase = 131072;                // start of the F region
+constexpr uint32_t kTBase = 147456;                // start of the T region
+constexpr int kImageCount = 2;                     // images: [0] RL = 16, [1] RL = 4
 
 constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
   return ((m >> 1) << 16) | (e << 8) | ((m & 1) << 7) | (c << 2);
@@ -39,5 +49,9 @@ constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
 constexpr uint32_t f_addr(uint32_t c, uint32_t nib, uint32_t v) {
   return kFBase | (nib << 11) | (v << 7) | (c << 2);
 }
+constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {
+  return kTBase + ((64u * h + 16u * t + v) << 7) + (c << 2);
+}
+constexpr int image_index(int rl) { return rl == 16 ? 0 : 1; }
 
 }  // namespace lnx

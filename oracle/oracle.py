@@ -167,6 +167,114 @@ def ipv6_pseudo(ip6: bytes) -> CRC791:
     return c
 
 
+# ------------------------------------------- receive-path checksum verdicts
+# lneto.errGeneric codes (errors.go:6-28) the receive path returns.
+ERR_PACKET_DROP = 2
+ERR_BAD_CRC = 3
+ERR_INVALID_FIELD = 14
+ERR_INVALID_LENGTH_FIELD = 15
+ERR_TRUNCATED_FRAME = 18
+VERIFY_EVIL_BIT = 1  # mirrors lneto.ValidateEvilBit on the stack's Validator
+
+ETHERTYPE_IPV4 = 0x0800
+ETHERTYPE_IPV6 = 0x86DD
+ETHERTYPE_VLAN = 0x8100
+IPPROTO_TCP = 6
+IPPROTO_UDP = 17
+
+
+def _be16(b: bytes, i: int) -> int:
+    return (b[i] << 8) | b[i + 1]
+
+
+def _ipv4_verdict(ip: bytes, flags: int) -> int:
+    """demux4 up to its checksum checks (internet/stack-ip4.go:100-164), with
+    every destination accepted and a handler for every protocol."""
+    if len(ip) < 20:                                   # ipv4.NewFrame (ipv4/frame.go:15-20)
+        return ERR_TRUNCATED_FRAME
+    # ValidateExceptCRC (ipv4/frame.go:229-238) on a Validator without
+    # validateAllowMultiErrors: the first error added wins (validation.go AddError).
+    tl, ihl, version = _be16(ip, 2), ip[0] & 0xF, ip[0] >> 4
+    errs = []
+    if tl < 20:                                        # ValidateSize (ipv4/frame.go:214-227)
+        errs.append(ERR_INVALID_LENGTH_FIELD)
+    if tl > len(ip):
+        errs.append(ERR_TRUNCATED_FRAME)
+    if ihl < 5 or ihl * 4 > tl:
+        errs.append(ERR_INVALID_LENGTH_FIELD)
+    if version != 4:
+        errs.append(ERR_INVALID_FIELD)
+    if flags & VERIFY_EVIL_BIT and _be16(ip, 6) & (1 << 13):  # Flags.IsEvil (ipv4/definitions.go:68-87)
+        errs.append(ERR_PACKET_DROP)
+    if errs:
+        return errs[0]
+    if ipv4_header_sum16(ip) != 0:                     # CalculateHeaderCRC: first 20 bytes only
+        return ERR_BAD_CRC
+    hl, proto = ihl * 4, ip[9]
+    payload = ip[hl:tl]                                # Frame.Payload (ipv4/frame.go:188-192)
+    if proto == IPPROTO_TCP:
+        if ipv4_tcp_pseudo(ip).payload_sum16(payload) != 0:
+            return ERR_BAD_CRC
+    elif proto == IPPROTO_UDP:
+        if len(payload) < 8:                           # udp.NewFrame (udp/frame.go:15-20)
+            return ERR_TRUNCATED_FRAME
+        ul = _be16(payload, 4)
+        if ul < 8:                                     # udp ValidateSize (udp/frame.go:96-104)
+            return ERR_INVALID_LENGTH_FIELD
+        if ul > len(payload):
+            return ERR_TRUNCATED_FRAME
+        if ipv4_udp_pseudo(ip, ul).payload_sum16(payload[:ul]) != 0:
+            return ERR_BAD_CRC
+    return 0
+
+
+def _ipv6_verdict(ip6: bytes) -> int:
+    """demux6 up to its checksum checks (internet/stack-ip6.go:86-138)."""
+    if len(ip6) < 40:                                  # ipv6.NewFrame (ipv6/frame.go:13-18)
+        return ERR_TRUNCATED_FRAME
+    pl = _be16(ip6, 4)
+    if pl + 40 > len(ip6):                             # ValidateSize (ipv6/frame.go:123-128)
+        return ERR_INVALID_LENGTH_FIELD
+    proto = ip6[6]
+    payload = ip6[40:40 + pl]                          # Frame.Payload (ipv6/frame.go:34-37)
+    if proto == IPPROTO_TCP:
+        if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
+            return ERR_BAD_CRC
+    elif proto == IPPROTO_UDP:
+        if len(payload) < 8:
+            return ERR_TRUNCATED_FRAME
+        ul = _be16(payload, 4)
+        if ul < 8:
+            return ERR_INVALID_LENGTH_FIELD
+        if ul > len(payload):
+            return ERR_TRUNCATED_FRAME
+        # quirk kept: the IPv6 UDP sum covers the whole IPv6 payload, not the UDP length
+        if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
+            return ERR_BAD_CRC
+    return 0
+
+
+def ingress_verdict(frame: bytes, flags: int = 0) -> int:
+    """Checksum-stage verdict of lneto's receive path for one Ethernet frame
+    (FCS stripped): StackEthernet.Demux (internet/stack-ethernet.go:139-165)
+    size checks, then demux4 / demux6 by EtherType.  0 = every check passed or
+    none applies (other EtherTypes); else the errGeneric code returned.
+    Destination filtering and handler lookup (ErrPacketDrop) are stack
+    configuration and are taken as accept-all."""
+    if len(frame) < 14:                                # ethernet.NewFrame (ethernet/frame.go:13-18)
+        return ERR_TRUNCATED_FRAME
+    et = _be16(frame, 12)
+    if et <= 1500 and len(frame) < et:                 # ValidateSize (ethernet/frame.go:119-127)
+        return ERR_INVALID_LENGTH_FIELD
+    if et == ETHERTYPE_VLAN and len(frame) < 18:
+        return ERR_TRUNCATED_FRAME
+    if et == ETHERTYPE_IPV4:
+        return _ipv4_verdict(frame[14:], flags)
+    if et == ETHERTYPE_IPV6:
+        return _ipv6_verdict(frame[14:])
+    return 0
+
+
 # ----------------------------------------------------------------- C oracle
 _lib = None
 

@@ -1,0 +1,132 @@
+// rows_emulator.cpp — CPU emulation of one row of crc32_rows_kernel, lane by
+// lane, reading the real LDS images that liblneto_amd builds (api.cpp
+// build_lds_image) at the byte addresses the kernel uses.  Checks the window
+// geometry (aligned window end, lead-in mask, init fold and its spill, junk
+// removal, F_p, row XOR, Z_{-t} fix) against a plain table CRC-32 for every
+// length 0..N at every start alignment and in every row of the wave, for both
+// row widths.  No GPU: this pins the algebra and the table contents on the CPU.
+// Built and run by tests/test_abi.py.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include "../../lneto_amd/csrc/lds_layout.hpp"
+
+namespace lnx {
+std::vector<uint32_t> build_lds_image(uint32_t rl);
+}
+using namespace lnx;
+
+static uint32_t crc_tab[256];
+static uint32_t ref_crc(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = crc_tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return ~c;
+}
+
+struct Emu {
+  int RL;
+  std::vector<uint32_t> img;
+  uint32_t rd(uint32_t byte_addr) const { return img[byte_addr / 4]; }
+  uint32_t U(uint32_t x, uint32_t c) const {  // u_step: byte m of x -> U_m
+    uint32_t r = 0;
+    for (uint32_t m = 0; m < 4; ++m) r ^= rd(u_addr(m, (x >> (8 * m)) & 0xFF, c));
+    return r;
+  }
+  uint32_t F(uint32_t r, uint32_t c) const {
+    uint32_t a = 0;
+    for (uint32_t i = 0; i < 8; ++i) a ^= rd(f_addr(c, i, (r >> (4 * i)) & 15));
+    return a;
+  }
+  // word at rel position pos of the wave's range [0, size): out-of-range reads 0
+  static uint32_t word(const std::vector<uint8_t>& buf, int64_t pos) {
+    if (pos < 0 || pos + 4 > (int64_t)buf.size()) return 0;
+    uint32_t w;
+    memcpy(&w, &buf[pos], 4);
+    return w;
+  }
+  static uint32_t keep_from(int32_t lo) {
+    lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+    return (uint32_t)(0xFFFFFFFFull << (8 * lo));
+  }
+  // CRC of frame [rs, re) of buf as row `row` of a wave would compute it.
+  uint32_t crc(const std::vector<uint8_t>& buf, uint32_t rs, uint32_t re, uint32_t row) const {
+    const uint32_t SB = 4 * RL;
+    const uint32_t n = re > rs ? re - rs : 0;
+    const uint32_t ea = (re + 3) & ~3u, t = ea - re;
+    const uint32_t J = n ? (n + t + SB - 1) / SB : 0;
+    const int64_t ws = (int64_t)ea - (int64_t)J * SB;
+    const uint32_t lead = J * SB - n - t;
+    std::vector<uint32_t> lanes(RL);
+    for (uint32_t p = 0; p < (uint32_t)RL; ++p) {
+      const uint32_t c = (row * RL + p) % 32;
+      const uint32_t m4 = n < 4 ? n : 4;
+      const int32_t d0 = (int32_t)lead - (int32_t)(4 * p);
+      const uint32_t keep = keep_from(d0), initm = keep & ~keep_from(d0 + (int32_t)m4);
+      const int32_t x1 = (int32_t)(lead + m4) - (int32_t)SB;
+      const uint32_t m1 = (x1 > 0 && p == 0) ? (uint32_t)((1ull << (8 * x1)) - 1) : 0;
+      uint32_t reg = 0;
+      for (uint32_t j = 0; j < J; ++j) {
+        uint32_t x = word(buf, ws + 4 * p + (int64_t)SB * j);
+        if (j == 0) x = (x & keep) ^ initm;
+        if (j == 1) x ^= m1;
+        reg = U(reg ^ x, c);
+      }
+      if (J && t && p == (uint32_t)RL - 1) {
+        const uint32_t junk = word(buf, (int64_t)ea - 4) & ~(uint32_t)(0xFFFFFFFFull >> (8 * t));
+        reg ^= U(junk, c);
+      }
+      lanes[p] = F(reg, c);
+    }
+    uint32_t R = 0;
+    for (uint32_t v : lanes) R ^= v;  // row_xor
+    // t_fix: lane-shared nibble lookups, XOR-reduced as the DPP steps do
+    uint32_t T = 0;
+    if (RL == 16) {
+      for (uint32_t p = 0; p < 8; ++p) {  // lanes 0-3 and 4-7 of the reduction of lane 0
+        const uint32_t c = (row * RL + p) % 32, q = p & 7;
+        T ^= rd(t_addr(c, 0, t, (R >> (4 * q)) & 15));
+      }
+    } else {
+      for (uint32_t p = 0; p < 4; ++p) {
+        const uint32_t c = (row * RL + p) % 32;
+        T ^= rd(t_addr(c, 0, t, (R >> (4 * p)) & 15)) ^ rd(t_addr(c, 1, t, (R >> (4 * p + 16)) & 15));
+      }
+    }
+    R = n ? T : 0;
+    if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    return ~R;
+  }
+};
+
+int main() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? 0xEDB88320u : 0);
+    crc_tab[i] = c;
+  }
+  std::vector<uint8_t> buf(8192);
+  uint64_t s = 0x6C6E65746FULL;
+  for (auto& b : buf) {
+    s = s * 6364136223846793005ULL + 1442695040888963407ULL;
+    b = (uint8_t)(s >> 56);
+  }
+  int bad = 0, checked = 0;
+  for (int rl : {16, 4}) {
+    Emu e{rl, build_lds_image((uint32_t)rl)};
+    const uint32_t nr = 64 / rl;
+    for (uint32_t n = 0; n <= 1100; ++n) {
+      for (uint32_t start : {0u, 1u, 2u, 3u, 61u, 130u, 4093u}) {
+        if (start + n > buf.size()) continue;
+        const uint32_t row = (n + start) % nr;
+        const uint32_t got = e.crc(buf, start, start + n, row);
+        const uint32_t want = ref_crc(&buf[start], n);
+        ++checked;
+        if (got != want && bad++ < 10)
+          printf("RL=%d n=%u start=%u row=%u: got %08x want %08x\n", rl, n, start, row, got, want);
+      }
+    }
+  }
+  printf("rows emulator: %d of %d frames wrong\n", bad, checked);
+  return bad ? 1 : 0;
+}

@@ -1,0 +1,151 @@
+"""Synthetic Ethernet/IPv4/IPv6/TCP/UDP frames with valid or broken checksums,
+shaped like lneto's own test generators (internal/ltesto/ltesto.go:99-135,209-228:
+Ethernet + IPv4 (IHL 5) + TCP/UDP with the checksums filled in), widened with IP
+options, IPv6, other protocols and the malformed cases demux4 / demux6 reject.
+
+Checksum fields are filled with the oracle restatement of crc.go / ipv4/frame.go /
+ipv6/frame.go (tests/test_oracle.py pins it on lneto_test.go:119-160)."""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+from oracle import oracle as O
+
+
+def ether(et: int, payload: bytes) -> bytes:
+    return bytes.fromhex("c0ffee00dead") + bytes.fromhex("4e8b3af9fb6b") + struct.pack(">H", et) + payload
+
+
+def ipv4(proto: int, l4: bytes, opts: bytes = b"", flags: int = 0x4000, fix_l4: bool = True) -> bytes:
+    ihl = 5 + len(opts) // 4
+    tl = ihl * 4 + len(l4)
+    hdr = bytearray(struct.pack(">BBHHHBBH4s4s", 0x40 | ihl, 0, tl, 0x1234, flags, 64, proto, 0,
+                                bytes([192, 168, 10, 1]), bytes([192, 168, 10, 2]))) + opts
+    hdr[10:12] = struct.pack(">H", O.ipv4_header_sum16(bytes(hdr)))  # covers 20 bytes only
+    l4 = bytearray(l4)
+    if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
+        l4[16:18] = b"\0\0"
+        l4[16:18] = struct.pack(">H", O.ipv4_tcp_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
+    if fix_l4 and proto == O.IPPROTO_UDP and len(l4) >= 8:
+        ul = struct.unpack(">H", l4[4:6])[0]
+        l4[6:8] = b"\0\0"
+        if ul <= len(l4):
+            l4[6:8] = struct.pack(">H", O.ipv4_udp_pseudo(bytes(hdr), ul).payload_sum16(bytes(l4[:ul])))
+    return bytes(hdr) + bytes(l4)
+
+
+def ipv6(proto: int, l4: bytes, fix_l4: bool = True) -> bytes:
+    hdr = bytearray(struct.pack(">IHBB", 0x60000000, len(l4), proto, 64)) + bytes(range(0x20, 0x40))
+    l4 = bytearray(l4)
+    if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
+        l4[16:18] = b"\0\0"
+        l4[16:18] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
+    if fix_l4 and proto == O.IPPROTO_UDP and len(l4) >= 8:
+        l4[6:8] = b"\0\0"  # the stack sums the whole payload (stack-ip6.go:133-134)
+        l4[6:8] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
+    return bytes(hdr) + bytes(l4)
+
+
+def tcp(payload: bytes) -> bytes:
+    return struct.pack(">HHIIBBHHH", 0xE70A, 80, 0x4060D5CC, 0, 0x50, 0x18, 0xFAF0, 0, 0) + payload
+
+
+def udp(payload: bytes, length: int | None = None) -> bytes:
+    ul = 8 + len(payload) if length is None else length
+    return struct.pack(">HHHH", 5353, 53, ul, 0) + payload
+
+
+def frames(seed: int = 1, count: int = 3000) -> list[bytes]:
+    """A mixed batch: valid frames of every kind plus every malformation the
+    receive path distinguishes, with random payload sizes (odd ones too)."""
+    rng = np.random.default_rng(seed)
+
+    def pay(lo=0, hi=1400):
+        return rng.integers(0, 256, size=int(rng.integers(lo, hi)), dtype=np.uint8).tobytes()
+
+    out = []
+    for i in range(count):
+        kind = i % 24
+        if kind == 0:
+            f = ether(0x0800, ipv4(6, tcp(pay())))
+        elif kind == 1:
+            f = ether(0x0800, ipv4(17, udp(pay())))
+        elif kind == 2:  # IP options: the header sum still covers 20 bytes only (ipv4/frame.go:144-146)
+            f = ether(0x0800, ipv4(6, tcp(pay()), opts=bytes(4 * int(rng.integers(1, 11)))))
+        elif kind == 3:
+            f = ether(0x86DD, ipv6(6, tcp(pay())))
+        elif kind == 4:
+            f = ether(0x86DD, ipv6(17, udp(pay())))
+        elif kind == 5:  # corrupted payload byte
+            b = bytearray(ether(0x0800, ipv4(int(rng.choice([6, 17])), tcp(pay(1)))))
+            b[int(rng.integers(34, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(b)
+        elif kind == 6:  # corrupted IPv4 header byte (not the length/version fields)
+            b = bytearray(ether(0x0800, ipv4(6, tcp(pay()))))
+            b[int(rng.choice([15, 18, 19, 22, 26, 27, 30, 33]))] ^= 0x10
+            f = bytes(b)
+        elif kind == 7:  # corrupted IPv6 payload
+            b = bytearray(ether(0x86DD, ipv6(int(rng.choice([6, 17])), udp(pay(1)))))
+            b[int(rng.integers(54, len(b)))] ^= 0x80
+            f = bytes(b)
+        elif kind == 8:  # UDP checksum 0 on IPv4: NOT special-cased by the stack (stack-ip4.go:152-167)
+            b = bytearray(ether(0x0800, ipv4(17, udp(pay()))))
+            b[40:42] = b"\0\0"
+            f = bytes(b)
+        elif kind == 9:  # other IP protocols: no transport sum
+            f = ether(0x0800, ipv4(1, pay(8)))
+        elif kind == 10:
+            f = ether(0x86DD, ipv6(58, pay(8)))
+        elif kind == 11:  # truncated total length: tl > buffer
+            b = bytearray(ether(0x0800, ipv4(6, tcp(pay()))))
+            b = b[: int(rng.integers(34, len(b)))]
+            f = bytes(b)
+        elif kind == 12:  # trailing bytes past tl (Ethernet padding): ignored
+            f = ether(0x0800, ipv4(17, udp(pay(0, 10)))) + bytes(int(rng.integers(1, 30)))
+        elif kind == 13:  # bad IHL / tl / version fields
+            b = bytearray(ether(0x0800, ipv4(6, tcp(pay()))))
+            m = int(rng.integers(0, 4))
+            if m == 0:
+                b[14] = 0x40 | int(rng.integers(0, 5))   # ihl < 5
+            elif m == 1:
+                b[16:18] = struct.pack(">H", int(rng.integers(0, 20)))  # tl < 20
+            elif m == 2:
+                b[14] = 0x60 | (b[14] & 15)              # version 6
+            else:
+                b[14] = 0x4F                             # ihl*4 = 60 > tl possibly
+            f = bytes(b)
+        elif kind == 14:  # evil bit (only rejected with VERIFY_EVIL_BIT)
+            f = ether(0x0800, ipv4(6, tcp(pay()), flags=0x2000))
+        elif kind == 15:  # UDP length field broken
+            ul = int(rng.choice([0, 3, 7, 9000]))
+            f = ether(0x0800, ipv4(17, udp(pay(), length=ul)))
+        elif kind == 16:  # IPv6 payload length too large / UDP too short
+            b = bytearray(ether(0x86DD, ipv6(17, udp(pay(0, 6)))))
+            if rng.integers(0, 2):
+                b[18:20] = struct.pack(">H", len(b))
+            else:
+                b = b[: 14 + 40 + int(rng.integers(0, 8))]
+                b[18:20] = struct.pack(">H", len(b) - 54)
+            f = bytes(b)
+        elif kind == 17:  # short frames
+            f = pay(0, 60)
+        elif kind == 18:  # VLAN, size-type, ARP EtherTypes
+            et = int(rng.choice([0x8100, 0x0806, 46, 1500, 0x88CC]))
+            f = ether(et, pay(0, 100))
+            if et == 0x8100 and rng.integers(0, 2):
+                f = f[: int(rng.integers(14, 18))]
+        elif kind == 19:  # IPv4 with a UDP payload shorter than the UDP header
+            f = ether(0x0800, ipv4(17, pay(0, 8), fix_l4=False))
+        elif kind == 20:  # random bytes behind IPv4 / IPv6 EtherTypes
+            f = ether(int(rng.choice([0x0800, 0x86DD])), pay(0, 200))
+        elif kind == 21:  # odd-length TCP segment (trailing byte weighted << 8)
+            f = ether(0x0800, ipv4(6, tcp(pay(1, 50) + b"\x7f")))
+        elif kind == 22:  # jumbo-ish
+            f = ether(0x0800, ipv4(6, tcp(pay(3000, 8900))))
+        else:  # minimum-size frame with Ethernet padding
+            f = ether(0x0800, ipv4(17, udp(b"")))
+            f = f + bytes(max(0, 60 - len(f)))
+        out.append(f)
+    return out

@@ -1,0 +1,61 @@
+"""Every CRC kernel configuration the dispatcher can pick, forced on every
+workgroup, is bit-exact against the oracle.
+
+The product dispatch (lnx_crc32_batch) chooses the row width per workgroup from
+its frames' mean length, so a given test batch exercises only some of the
+compiled configurations.  The profiling entry point lnx__crc32_variant forces
+one configuration for the whole launch (ids in crc32_kernel.hip launch_rows).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import lneto_amd as L
+from lneto_amd import synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# 20/21: 16-lane rows (KS, S) = (24, 2), (12, 3); 22..25: 4-lane rows (8,3), (16,3), (12,2), (6,3)
+FORCED = [20, 21, 22, 23, 24, 25]
+
+L.lib.lnx__crc32_variant.restype = ctypes.c_int
+L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+
+
+def _run(var, d, o, n):
+    import torch
+    out = torch.empty(n, dtype=torch.int32, device=d.device)
+    rc = L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def _batches(cuda):
+    import torch
+    rng = np.random.default_rng(5)
+    # every length 0..700 shuffled, after a 3-byte pad: all lead-ins, all end alignments
+    lens = rng.permutation(np.arange(0, 701))
+    off = synth.offsets_from_lengths(lens) + 3
+    off = np.concatenate([[0], off]).astype(np.uint64)  # frame 0 is the 3-byte pad
+    yield "lengths", off
+    yield "zipf", synth.offsets_from_lengths(synth.zipf_lengths(1 << 15, seed=77))
+    yield "long", synth.offsets_from_lengths(np.array([1, 2, 3, 5, 4097, 9001, 65537, 1500, 1499, 1498, 1497]))
+
+
+@pytest.mark.parametrize("var", FORCED)
+def test_forced_configuration_parity(cuda, var):
+    import torch
+    for name, off in _batches(cuda):
+        n = len(off) - 1
+        data = synth.bytes_np(int(off[-1]) + 8, seed=0xC0FFEE + n)
+        d = torch.from_numpy(data).to(cuda)
+        o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+        got = _run(var, d, o, n)
+        want = O.crc32_frames(data, off, threads=8)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"{name}: variant {var} wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]})"

@@ -1,0 +1,125 @@
+"""Receive-path checksum verdicts: the oracle restatement
+of StackEthernet.Demux -> demux4 / demux6 pinned on the reference's own frames
+and its documented quirks (CPU), and the fused HIP kernel
+lnx_ingress_verify_batch against it (GPU)."""
+import collections
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import framegen as G
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _kat_frames():
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "vectors.json")))
+    return [bytes.fromhex(f["frame"]) for f in g["lneto_tcp_frames"]]
+
+
+def test_reference_tcp_frames_pass():
+    """lneto_test.go:119-160 frames carry valid IPv4 and TCP checksums."""
+    for f in _kat_frames():
+        assert O.ingress_verdict(f) == 0
+
+
+def test_reference_tcp_frames_corrupted():
+    for f in _kat_frames():
+        for i in (15, 24, 26, 40, 50, 73):  # ToS, header CRC, src addr, TCP seq, TCP CRC, options
+            b = bytearray(f)
+            b[i] ^= 0x01
+            assert O.ingress_verdict(bytes(b)) == O.ERR_BAD_CRC, i
+
+
+def test_validation_order_and_codes():
+    ok4 = G.ether(0x0800, G.ipv4(6, G.tcp(b"hello")))
+    assert O.ingress_verdict(ok4) == 0
+    assert O.ingress_verdict(ok4[:13]) == O.ERR_TRUNCATED_FRAME            # ethernet.NewFrame
+    assert O.ingress_verdict(G.ether(1000, b"x" * 10)) == O.ERR_INVALID_LENGTH_FIELD  # size field > frame
+    assert O.ingress_verdict(G.ether(46, b"x" * 60)) == 0                  # size-type frame: no IP
+    assert O.ingress_verdict(G.ether(0x8100, b"ab")) == O.ERR_TRUNCATED_FRAME
+    assert O.ingress_verdict(ok4[:14 + 19]) == O.ERR_TRUNCATED_FRAME       # ipv4.NewFrame
+    b = bytearray(ok4); b[16:18] = struct.pack(">H", 19)
+    assert O.ingress_verdict(bytes(b)) == O.ERR_INVALID_LENGTH_FIELD       # tl < 20 (first error)
+    assert O.ingress_verdict(ok4[:-1]) == O.ERR_TRUNCATED_FRAME            # tl > len
+    b = bytearray(ok4); b[14] = 0x44
+    assert O.ingress_verdict(bytes(b)) == O.ERR_INVALID_LENGTH_FIELD       # ihl < 5
+    b = bytearray(ok4); b[14] = 0x65
+    assert O.ingress_verdict(bytes(b)) == O.ERR_INVALID_FIELD              # version != 4
+    evil = G.ether(0x0800, G.ipv4(6, G.tcp(b""), flags=0x2000))
+    assert O.ingress_verdict(evil) == 0
+    assert O.ingress_verdict(evil, O.VERIFY_EVIL_BIT) == O.ERR_PACKET_DROP
+    assert O.ingress_verdict(G.ether(0x0800, G.ipv4(17, b"1234567", fix_l4=False))) == O.ERR_TRUNCATED_FRAME
+    assert O.ingress_verdict(G.ether(0x0800, G.ipv4(17, G.udp(b"", length=7)))) == O.ERR_INVALID_LENGTH_FIELD
+    assert O.ingress_verdict(G.ether(0x0800, G.ipv4(17, G.udp(b"ab", length=11)))) == O.ERR_TRUNCATED_FRAME
+    ok6 = G.ether(0x86DD, G.ipv6(17, G.udp(b"payload")))
+    assert O.ingress_verdict(ok6) == 0
+    assert O.ingress_verdict(ok6[:14 + 39]) == O.ERR_TRUNCATED_FRAME
+    assert O.ingress_verdict(ok6[:-1]) == O.ERR_INVALID_LENGTH_FIELD       # pl + 40 > len
+
+
+def test_quirks_kept():
+    # UDP checksum 0 is not special-cased on receive (internet/stack-ip4.go:152-167)
+    b = bytearray(G.ether(0x0800, G.ipv4(17, G.udp(b"data"))))
+    b[40:42] = b"\0\0"
+    assert O.ingress_verdict(bytes(b)) == O.ERR_BAD_CRC
+    # IPv4 options are outside the header sum (ipv4/frame.go:144-146): flipping
+    # an option byte breaks nothing the receive path checks
+    b = bytearray(G.ether(0x0800, G.ipv4(6, G.tcp(b"x"), opts=b"\x01\x01\x01\x00")))
+    b[34] ^= 0x40
+    assert O.ingress_verdict(bytes(b)) == 0
+    # IPv6 UDP sums the whole IPv6 payload, not the UDP length (stack-ip6.go:133-134):
+    # bytes after the UDP length still count
+    b = bytearray(G.ether(0x86DD, G.ipv6(17, G.udp(b"abcdef", length=10))))
+    b[-1] ^= 0x01
+    assert O.ingress_verdict(bytes(b)) == O.ERR_BAD_CRC
+
+
+def test_generator_covers_every_verdict():
+    hist = collections.Counter(O.ingress_verdict(f, O.VERIFY_EVIL_BIT) for f in G.frames(count=2400))
+    for code in (0, O.ERR_PACKET_DROP, O.ERR_BAD_CRC, O.ERR_INVALID_FIELD, O.ERR_INVALID_LENGTH_FIELD,
+                 O.ERR_TRUNCATED_FRAME):
+        assert hist[code] > 0, (code, hist)
+
+
+def _pack(frames, base_pad):
+    parts, offs, pos = [b"\xAA" * base_pad], [base_pad], base_pad
+    for f in frames:
+        parts.append(f)
+        pos += len(f)
+        offs.append(pos)
+    return np.frombuffer(b"".join(parts) + b"\0" * 8, dtype=np.uint8).copy(), np.array(offs, dtype=np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base_pad", [0, 1, 2, 3])
+@pytest.mark.parametrize("flags", [0, 1])
+def test_gpu_ingress_verdicts_match_oracle(cuda, base_pad, flags):
+    import torch
+    import lneto_amd as L
+    frames = G.frames(seed=10 + base_pad, count=4800)
+    data, off = _pack(frames, base_pad)
+    d = torch.from_numpy(data).to(cuda)
+    o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+    got = L.ingress_verify_batch(d, o, flags=flags).cpu().numpy()
+    want = np.array([O.ingress_verdict(f, flags) for f in frames], dtype=np.uint8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
+
+
+@pytest.mark.gpu
+def test_gpu_ingress_reference_frames(cuda):
+    import torch
+    import lneto_amd as L
+    frames = _kat_frames()
+    frames += [bytes(b) for b in (bytearray(frames[0]),)]
+    bad = bytearray(frames[1]); bad[60] ^= 0x20
+    frames.append(bytes(bad))
+    data, off = _pack(frames, 0)
+    got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda),
+                                 torch.from_numpy(off.astype(np.int64)).to(cuda)).cpu().numpy()
+    assert got.tolist() == [0, 0, 0, O.ERR_BAD_CRC]

@@ -4,6 +4,7 @@
 // Frames are packed back to back; each wave owns a contiguous range of frames.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <vector>
 #include <algorithm>
@@ -54,9 +55,10 @@ float tm(F fn) {
   std::sort(t.begin(), t.end()); return t[3];
 }
 
-int main() {
-  const uint32_t fb = 1536;  // frame bytes (multiple of 256 so every pattern tiles it)
-  const uint64_t nframes = 1 << 20;
+int main(int argc, char** argv) {
+  // frame bytes (default 1536, a multiple of 256 so every pattern tiles it)
+  const uint32_t fb = argc > 1 ? (uint32_t)atoi(argv[1]) : 1536;
+  const uint64_t nframes = (1536ull << 20) / fb;
   uint8_t* buf; uint32_t* out;
   (void)hipMalloc(&buf, nframes * fb); (void)hipMalloc(&out, 64);
   (void)hipMemset(buf, 3, nframes * fb);
@@ -67,5 +69,6 @@ int main() {
   RUN(8, 4, 6); RUN(8, 4, 12);
   RUN(16, 4, 3); RUN(16, 4, 6);
   RUN(4, 1, 6); RUN(16, 1, 1); RUN(16, 2, 3);
+  RUN(4, 8, 6); RUN(4, 8, 12); RUN(4, 16, 8); RUN(4, 16, 16); RUN(8, 16, 4); RUN(8, 16, 8);
   return 0;
 }
