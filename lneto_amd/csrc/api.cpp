@@ -15,7 +15,8 @@ namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                bool verify, const void* image, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* image, int num_cus, hipStream_t stream);
+                                const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
+uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
@@ -39,7 +40,7 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
         img[f_addr(c, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * p);  // F_p = Z_{-4p}
     const uint32_t q0 = (uint32_t)p & 7u;
     for (uint32_t h = 0; h < 2; ++h)
-      for (uint32_t t = 0; t < 4; ++t)
+      for (uint32_t t = 1; t < 4; ++t)
         for (uint32_t v = 0; v < 16; ++v)
           img[t_addr(c, h, t, v) / 4] = zshift_bytes(v << (4 * (q0 + 4 * h)), -(int64_t)t);  // Z_{-t}
   }
@@ -221,8 +222,24 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream));
+                                      static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
+  return LNX_OK;
+}
+
+// Profiling hook: the variant with a per-wave timeline (3 x uint64 per wave:
+// entry, image copied, exit; 100 MHz clock).  Returns the wave count when
+// d_timeline is NULL.
+int64_t lnx__crc32_timeline(int var, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
+                            uint64_t* d_timeline, void* stream) {
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  if (!d_timeline) return (int64_t)crc32_launch_waves(n, c->num_cus);
+  if (n == 0 || !d_bytes || !d_off || !d_crc) return LNX_EINVAL;
+  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream), d_timeline);
+  if (e != hipSuccess) return hip_fail(e, "crc32 timeline launch");
   return LNX_OK;
 }
 

@@ -115,19 +115,23 @@ __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
   return v;
 }
 
-// Z_{-t}(R) for a row-uniform R, the nibbles shared over the row (T region).
+// Z_{-t}(R) for a row-uniform R, the nibbles shared over the row (T region);
+// t = 0 is the identity: each lane then contributes its nibbles in place.
 template <int RL>
 __device__ __forceinline__ uint32_t t_fix(const char* lds, uint32_t R, uint32_t t, uint32_t p, uint32_t bt) {
+  const uint32_t tb = bt + (((t - 1u) & 3u) << 11);  // entry (h, t, v) = 48h + 16(t-1) + v, stride 128 B
   if constexpr (RL == 16) {
     const uint32_t q = p & 7u;  // lanes p and p+8 cover the same nibble
-    uint32_t a = lds_rd(lds, bt + (((t << 4) | ((R >> (4 * q)) & 15u)) << 7));
+    const uint32_t nib = (R >> (4 * q)) & 15u;
+    const uint32_t a0 = lds_rd(lds, tb + (nib << 7));
+    uint32_t a = t ? a0 : nib << (4 * q);
     a = dpp_xor<kQuadX1>(a);
     a = dpp_xor<kQuadX2>(a);
     return dpp_xor<kRowRor4>(a);  // quads {0-3,4-7}, {4-7,8-11}, ... : 8 distinct nibbles
   } else {
-    const uint32_t a0 = lds_rd(lds, bt + (((t << 4) | ((R >> (4 * p)) & 15u)) << 7));
-    const uint32_t a1 = lds_rd(lds, bt + ((64u | (t << 4) | ((R >> (4 * p + 16)) & 15u)) << 7));
-    uint32_t a = a0 ^ a1;
+    const uint32_t n0 = (R >> (4 * p)) & 15u, n1 = (R >> (4 * p + 16)) & 15u;
+    const uint32_t a0 = lds_rd(lds, tb + (n0 << 7)) ^ lds_rd(lds, tb + ((48u + n1) << 7));
+    uint32_t a = t ? a0 : (n0 << (4 * p)) | (n1 << (4 * p + 16));
     a = dpp_xor<kQuadX1>(a);
     return dpp_xor<kQuadX2>(a);
   }
@@ -204,11 +208,11 @@ __device__ __forceinline__ void ld_item(uint32_t* w, uint32_t v, __amdgpu_buffer
 // vmcnt wait naming every register of one slot: the wait, then empty asm
 // statements that "redefine" each register, so no use is scheduled above it.
 template <int N, int KS>
-__device__ __forceinline__ void slot_wait(uint32_t (&w)[KS], uint32_t& junk, uint32_t& bnd) {
+__device__ __forceinline__ void slot_wait(uint32_t (&w)[KS], uint32_t& junk, uint32_t& b0, uint32_t& b1) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N));
 #pragma unroll
   for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(w[k]));
-  asm volatile("" : "+v"(junk), "+v"(bnd));
+  asm volatile("" : "+v"(junk), "+v"(b0), "+v"(b1));
 }
 
 enum class CrcMode : int { kCrc = 0, kVerify = 1 };
@@ -270,43 +274,69 @@ __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* byt
 }
 
 // ------------------------------------------------------------------ ring body
-// Wave-uniform context of the pipelined path.
+// Workgroup-uniform context of the pipelined path.  Positions are
+// rel(x) = x - off[fb0] + adj, frame indices relative to fb0.
 struct WaveCtx {
-  uint32_t nwf, o0_lo, adj;
+  uint32_t nfb, o0_lo, adj;  // frames of the workgroup, low dword of off[fb0], alignment
+  uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase)
   __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc;
 };
 
-// RL: lanes per row, KS: window steps per item, S: ring slots, VAR: profiling
-// knob (0 = product, 1 = loads + bookkeeping only, 2 = lookups
-// + bookkeeping on synthetic words).  Only VAR 0 is reachable from the C-ABI.
-template <CrcMode MODE, int RL, int KS, int S, int VAR>
+// RL: lanes per row, KS: window steps per item, S: ring slots, CH: frames per
+// chunk, VAR: profiling knob (0 = product, 1 = loads +
+// bookkeeping only, 2 = lookups + bookkeeping on synthetic words).  Only VAR 0
+// is reachable from the C-ABI.
+//
+// Work distribution: the waves of a workgroup claim chunks of CH consecutive
+// frames from an LDS counter (one ds_add_rtn per chunk), so a wave that the
+// memory system serves faster simply takes more chunks; with static ranges the
+// waves of one CU finished up to 1.5x apart (tools/prof/timeline.py).  A wave
+// sees its chunks as one virtual frame sequence v = 0, 1, ...: it holds the
+// bases of the chunk v is in (bc) and of the next one (bn), which covers the
+// S*NR-frame bounds window every slot prefetches.
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
   constexpr uint32_t kSbLog = RL == 16 ? 6 : 4;
   static_assert(RL == 4 || RL == 16, "row width");
-  static_assert(S >= 2 && S * NR + 1 <= 64, "bounds prefetch window");
+  static_assert(S >= 2 && S * NR <= (uint32_t)CH && CH <= 64, "bounds window within two chunks");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
-  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 2;  // per slot: steps, junk word, bounds
+  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3;  // per slot: steps, junk word, frame start + end
   constexpr int kPending = (S - 1) * kLoads;       // loads issued after a slot's own
   const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bf = L.bf, bt = L.bt;
-  const uint32_t nwf = cx.nwf, o0_lo = cx.o0_lo, adj = cx.adj;
+  const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
   const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
 
-  // ---- per-row cursor (row-uniform VGPRs); positions are rel(x) = x - off[fw0] + adj
-  uint32_t rf = kNoFrame;   // frame index relative to fw0
+  // ---- chunks (uniform)
+  auto claim = [&]() -> uint32_t {
+    uint32_t b = 0;
+    if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, (uint32_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+  };
+  uint32_t cc = 0;          // virtual chunk index of bc
+  uint32_t bc = claim();    // first frame of chunk cc
+  uint32_t bn = claim();    // first frame of chunk cc + 1
+  auto vframe = [&](uint32_t v) -> uint32_t {  // frame of virtual index v, kNoFrame past the work
+    const uint32_t c0 = cc * CH;
+    const uint32_t f = v < c0 + CH ? bc + (v - c0) : (v < c0 + 2 * CH ? bn + (v - c0 - CH) : kNoFrame);
+    return f < nfb ? f : kNoFrame;
+  };
+
+  // ---- per-row cursor (row-uniform VGPRs)
+  uint32_t rf = kNoFrame;   // frame index
   uint32_t rea = 0;         // rel(end) rounded up to 4: the window end
   uint32_t rn = 0, rt = 0;  // length, window bytes past the frame end
   uint32_t rJ = 0, rj = 0;  // steps of the frame, next step to issue
-  uint32_t nf = 0;          // next unassigned frame of the wave (uniform)
+  uint32_t nf = 0;          // next unassigned virtual frame of the wave (uniform)
 
   // ---- ring slots
   uint32_t w[S][KS];
-  uint32_t jk[S];   // the last lane's last word (junk bytes past the frame end)
-  uint32_t bnd[S];  // lane i: low dword of off[fw0 + nfb[s] + i]
-  uint32_t nfb[S];  // uniform
+  uint32_t jk[S];             // the last lane's last word (junk bytes past the frame end)
+  uint32_t fi[S], sb[S], eb[S];  // lane i: frame of virtual index nfv[s] + i, its start / end (low dwords)
+  uint32_t nfv[S];            // uniform
   uint32_t it_f[S], it_n[S], it_t[S], it_j0[S], it_ns[S];
-  bool hw[S];       // uniform: slot holds work
+  bool hw[S];                 // uniform: slot holds work
 #pragma unroll
   for (int s = 0; s < S; ++s) {
 #pragma unroll
@@ -315,14 +345,16 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     it_f[s] = kNoFrame;
     it_n[s] = it_t[s] = it_j0[s] = it_ns[s] = 0;
     hw[s] = false;
-    nfb[s] = 0;
+    nfv[s] = 0;
   }
   // first bounds window for every slot (drained before the loop)
   {
-    uint32_t b = ld_buf<0>(lane * 8u, off_rsrc);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(b));
+    const uint32_t f = vframe(lane);
+    const uint32_t o = f != kNoFrame ? f * 8u : kOOB;
+    uint32_t a = ld_buf<0>(o, off_rsrc), b = ld_buf<8>(o, off_rsrc);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b));
 #pragma unroll
-    for (int s = 0; s < S; ++s) bnd[s] = b;
+    for (int s = 0; s < S; ++s) fi[s] = f, sb[s] = a, eb[s] = b;
   }
 
   uint32_t reg = 0;  // this lane's CRC register for its row's frame in progress
@@ -336,16 +368,16 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     const uint64_t below = (1ull << (RL * row)) - 1;
     const uint32_t rank = (uint32_t)__builtin_popcountll(nmask & below);
     const uint32_t cnt = (uint32_t)__builtin_popcountll(nmask);
-    const uint32_t idx = nf + rank;
-    const uint32_t li = idx - nfb[s];  // <= S*NR - 1 by construction
-    const uint32_t s_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)bnd[s]);
-    const uint32_t e_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((li + 1) * 4u), (int)bnd[s]);
+    const uint32_t li = nf + rank - nfv[s];  // < S*NR by construction
+    const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)fi[s]);
+    const uint32_t s_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)sb[s]);
+    const uint32_t e_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)eb[s]);
     if (need) {
-      if (idx < nwf) {
+      if (f != kNoFrame) {
         const uint32_t len = e_lo - s_lo;
         const uint32_t n = (int32_t)len > 0 ? len : 0u;  // end below start: empty frame
         const uint32_t re = e_lo - o0_lo + adj;
-        rf = idx;
+        rf = f;
         rea = (re + 3u) & ~3u;
         rt = rea - re;
         rn = n;
@@ -356,7 +388,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         rJ = rj = 0;
       }
     }
-    nf = nf + cnt < nwf ? nf + cnt : nwf;
+    nf += cnt;
     // 2. the item of this slot
     const bool alive = rf != kNoFrame;
     const uint32_t left = rJ - rj;
@@ -367,8 +399,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     it_j0[s] = rj;
     it_ns[s] = ns;
     hw[s] = wave_any(alive);
-    // 3. streaming loads: w[k] = step rj + k from one base (negative for the
-    // wave's first frame's lead-in: those words read 0)
+    // 3. streaming loads: w[k] = step rj + k from one base (negative for a
+    // lead-in before the workgroup's first byte: those words read 0)
     const uint32_t voff = alive ? rea - ((rJ - rj) << kSbLog) + (p << 2) : kOOB;
     const bool ends = alive && rj + ns == rJ && rJ != 0;
     const uint32_t jv = ends && p == RL - 1 && rt != 0 ? rea - 4u : kOOB;
@@ -380,14 +412,23 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       ld_item<0, KS, (int)SB>(w[s], voff, data_rsrc);
     }
     jk[s] = ld_buf<0>(jv, data_rsrc);
-    // 4. bounds of the next S*NR+1 frames, for this slot's next issue
-    nfb[s] = nf;
-    bnd[s] = ld_buf<0>((nf + lane) * 8u, off_rsrc);
+    // 4. bounds of the next S*NR frames, for this slot's next issue
+    if (nf >= (cc + 1) * CH) {  // at most one chunk boundary per issue (cnt <= NR <= CH)
+      ++cc;
+      bc = bn;
+      bn = claim();
+    }
+    const uint32_t g = vframe(nf + lane);
+    const uint32_t go = g != kNoFrame ? g * 8u : kOOB;
+    nfv[s] = nf;
+    fi[s] = g;
+    sb[s] = ld_buf<0>(go, off_rsrc);
+    eb[s] = ld_buf<8>(go, off_rsrc);
   };
 
   auto compute = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
-    slot_wait<kPending, KS>(w[s], jk[s], bnd[s]);
+    slot_wait<kPending, KS>(w[s], jk[s], sb[s], eb[s]);
     const uint32_t n = it_n[s], t = it_t[s], ns = it_ns[s], j0 = it_j0[s];
     const uint32_t J = n ? (n + t + SB - 1) >> kSbLog : 0u;
     const bool alive = it_f[s] != kNoFrame;
@@ -452,7 +493,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     if (done) return;
     compute(sc);
     live -= hw[s] ? 1 : 0;
-    const bool more = nf < nwf || wave_any(rj < rJ);
+    const bool more = vframe(nf) != kNoFrame || wave_any(rj < rJ);
     if (live == 0 && !more) {
       done = true;
       return;
@@ -474,21 +515,25 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 
 // ------------------------------------------------------------------ kernel
 // Row width per workgroup from its frames' mean length (RLF = 0), or forced
-// (RLF = 4 / 16, profiling); item size and ring depth per row width.
-template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 2, int KS4 = 8, int S4 = 3>
+// (RLF = 4 / 16, profiling); item size, ring depth and chunk per row width.
+template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 2, int KS4 = 8, int S4 = 3,
+          int CH16 = 16, int CH4 = 64>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
-                  uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out) {
+                  uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
+                  uint64_t* __restrict__ timeline) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
+  // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
+  // after the LDS image copy and at exit; null in the product path
+  const uint64_t t_entry = timeline ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint64_t per_block = frames_per_wave * kWavesPerBlock;
   const uint64_t fb0 = (uint64_t)blockIdx.x * per_block < nframes ? (uint64_t)blockIdx.x * per_block : nframes;
   const uint64_t fb1 = fb0 + per_block < nframes ? fb0 + per_block : nframes;
+  const uint64_t ob0 = off[fb0], ob1 = off[fb1];
   bool narrow = RLF == 4;
-  if constexpr (RLF == 0) {
-    const uint64_t ob0 = off[fb0], ob1 = off[fb1];
-    narrow = fb1 > fb0 && ob1 > ob0 && ob1 - ob0 < kShortMean * (fb1 - fb0);
-  }
+  if constexpr (RLF == 0) narrow = fb1 > fb0 && ob1 > ob0 && ob1 - ob0 < kShortMean * (fb1 - fb0);
   {
+    // the image is zero at kCtrBase, which starts the chunk counter at 0
     const uint4* img = images + (narrow ? image_index(4) : image_index(16)) * (kLdsBytes / 16);
     uint4* l4 = reinterpret_cast<uint4*>(lds_words);
 #pragma unroll
@@ -505,20 +550,23 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   L.bf = kFBase | (col << 2);
   L.bt = kTBase | (col << 2);
   const uint64_t gwave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
-  const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
-  const uint32_t nwf = (uint32_t)(fw1 - fw0);
   __syncthreads();
   const char* lds = reinterpret_cast<const char*>(lds_words);
-  if (nwf == 0) return;
+  uint64_t* tl = nullptr;
+  if (timeline) {
+    tl = timeline + 3 * gwave;
+    if (lane == 0) tl[0] = t_entry, tl[1] = __builtin_amdgcn_s_memrealtime(), tl[2] = 0;
+  }
+  if (fb1 == fb0) return;
 
-  // The wave's byte range, addressed through one buffer descriptor whose base
-  // is 4-byte aligned: rel(x) = x - off[fw0] + adj.
-  const uint64_t o0 = off[fw0];
-  const uint64_t o1 = off[fw1];
-  const uint64_t range = o1 > o0 ? o1 - o0 : 0;  // non-decreasing offsets are the contract
-  const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + o0) & 3u);
+  // The workgroup's byte range, addressed through one buffer descriptor whose
+  // base is 4-byte aligned: rel(x) = x - off[fb0] + adj.
+  const uint64_t range = ob1 > ob0 ? ob1 - ob0 : 0;  // non-decreasing offsets are the contract
+  const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + ob0) & 3u);
   if (range + adj + 4096 >= (1ull << 31)) {
+    // gigabyte frames: static per-wave ranges on the unpipelined path
+    const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
+    const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_generic<MODE, 4>(lds, L, bytes, off, fw0, fw1, out);
@@ -526,31 +574,34 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       L.p = lane & 15u, L.row = lane >> 4;
       rows_generic<MODE, 16>(lds, L, bytes, off, fw0, fw1, out);
     }
+    if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
     return;
   }
   WaveCtx cx;
-  cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + o0 - adj), (short)0,
+  cx.nfb = (uint32_t)(fb1 - fb0);
+  cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + ob0 - adj), (short)0,
                                                    (int)((range + adj + 3) & ~3ull), 0x00020000);
-  cx.off_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(off + fw0), (short)0,
-                                                  (int)((nwf + 1) * 8u), 0x00020000);
+  cx.off_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(off + fb0), (short)0,
+                                                  (int)((cx.nfb + 1) * 8u), 0x00020000);
   constexpr uint32_t elem = MODE == CrcMode::kCrc ? 4u : 1u;
-  cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + fw0 * elem, (short)0,
-                                                  (int)(nwf * elem), 0x00020000);
-  cx.nwf = nwf;
-  cx.o0_lo = (uint32_t)o0;
+  cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + fb0 * elem, (short)0,
+                                                  (int)(cx.nfb * elem), 0x00020000);
+  cx.o0_lo = (uint32_t)ob0;
   cx.adj = adj;
+  cx.ctr = lds_words + kCtrBase / 4;
   asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
   if (narrow) {
     L.p = lane & 3u, L.row = lane >> 2;
-    rows_body<MODE, 4, KS4, S4, VAR>(lds, L, cx);
+    rows_body<MODE, 4, KS4, S4, CH4, VAR>(lds, L, cx);
   } else {
     L.p = lane & 15u, L.row = lane >> 4;
-    rows_body<MODE, 16, KS16, S16, VAR>(lds, L, cx);
+    rows_body<MODE, 16, KS16, S16, CH16, VAR>(lds, L, cx);
   }
+  if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                       const void* images, int num_cus, hipStream_t stream) {
+                       const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
   uint64_t grid = (n + per_block - 1) / per_block;
@@ -560,7 +611,7 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const uint4* img = static_cast<const uint4*>(images);
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
-  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out)
+  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, timeline)
   if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
@@ -570,6 +621,8 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;              // lookups + bookkeeping only
       case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3); break;
+      case 28: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 8); break;   // 8-frame chunks
+      case 29: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 32); break;  // 32-frame chunks
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 8, 3); break;  // forced 4-lane rows
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 16, 3); break;
       case 24: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 12, 2); break;
@@ -589,8 +642,15 @@ hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64
   return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream);
 }
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream);
+                                const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
+  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, timeline);
+}
+// Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
+uint64_t crc32_launch_waves(uint64_t n, int num_cus) {
+  const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;
+  uint64_t grid = (n + per_block - 1) / per_block;
+  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+  return grid * kWavesPerBlock;
 }
 
 }  // namespace lnx

@@ -26,12 +26,16 @@
 // F_p(r) = XOR_i F_p,i[(r >> 4i) & 15]; column c holds the tables of
 // p = c % RL, which serves lanes c and c+32 alike.
 //
-// T region [144 KiB, 160 KiB): the window ends at the frame end rounded up to
+// T region [144 KiB, 156 KiB): the window ends at the frame end rounded up to
 // 4 bytes, t = 0..3 bytes past it, so the row's register needs Z_{-t} too.  The
-// row's lanes share that work by nibble: entry (h, t, v) of column c is
-// Z_{-t}(v << 4q_h) with q_0 = (c % RL) & 7 and q_1 = q_0 + 4 (h = 1 is used
-// by RL = 4 only, where each lane covers two nibbles):
-//     byte address = 144K | (64h + 16t + v)<<7 | c<<2
+// row's lanes share that work by nibble: entry (h, t, v) of column c, t = 1..3,
+// is Z_{-t}(v << 4q_h) with q_0 = (c % RL) & 7 and q_1 = q_0 + 4 (h = 1 is used
+// by RL = 4 only, where each lane covers two nibbles); t = 0 is the identity
+// and needs no table:
+//     byte address = 144K | (48h + 16(t-1) + v)<<7 | c<<2
+//
+// [156 KiB, 160 KiB): zero in the image; the workgroup's frame-chunk counter
+// lives at kCtrBase (DESIGN.md §3.1 "work distribution").
 #pragma once
 #include <cstdint>
 
@@ -41,6 +45,7 @@ constexpr uint32_t kLdsBytes = 163840;             // 160 KiB (whole CU)
 constexpr uint32_t kLdsDwords = kLdsBytes / 4;
 constexpr uint32_t kFBase = 131072;                // start of the F region
 constexpr uint32_t kTBase = 147456;                // start of the T region
+constexpr uint32_t kCtrBase = 159744;              // frame-chunk counter (one dword)
 constexpr int kImageCount = 2;                     // images: [0] RL = 16, [1] RL = 4
 
 constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
@@ -49,9 +54,10 @@ constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
 constexpr uint32_t f_addr(uint32_t c, uint32_t nib, uint32_t v) {
   return kFBase | (nib << 11) | (v << 7) | (c << 2);
 }
-constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {
-  return kTBase + ((64u * h + 16u * t + v) << 7) + (c << 2);
+constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // t = 1..3
+  return kTBase + ((48u * h + 16u * (t - 1) + v) << 7) + (c << 2);
 }
+static_assert(t_addr(31, 1, 3, 15) < kCtrBase, "T region overlaps the counter");
 constexpr int image_index(int rl) { return rl == 16 ? 0 : 1; }
 
 }  // namespace lnx

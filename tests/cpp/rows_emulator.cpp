@@ -82,15 +82,19 @@ struct Emu {
     for (uint32_t v : lanes) R ^= v;  // row_xor
     // t_fix: lane-shared nibble lookups, XOR-reduced as the DPP steps do
     uint32_t T = 0;
+    auto tl = [&](uint32_t c, uint32_t h, uint32_t q) {  // t = 0: identity, no table
+      const uint32_t nib = (R >> (4 * q)) & 15;
+      return t ? rd(t_addr(c, h, t, nib)) : nib << (4 * q);
+    };
     if (RL == 16) {
       for (uint32_t p = 0; p < 8; ++p) {  // lanes 0-3 and 4-7 of the reduction of lane 0
-        const uint32_t c = (row * RL + p) % 32, q = p & 7;
-        T ^= rd(t_addr(c, 0, t, (R >> (4 * q)) & 15));
+        const uint32_t c = (row * RL + p) % 32;
+        T ^= tl(c, 0, p & 7);
       }
     } else {
       for (uint32_t p = 0; p < 4; ++p) {
         const uint32_t c = (row * RL + p) % 32;
-        T ^= rd(t_addr(c, 0, t, (R >> (4 * p)) & 15)) ^ rd(t_addr(c, 1, t, (R >> (4 * p + 16)) & 15));
+        T ^= tl(c, 0, p) ^ tl(c, 1, p + 4);
       }
     }
     R = n ? T : 0;
