@@ -9,7 +9,9 @@ lnx_crc32_batch call over the rank's whole frame batch (inputs already in HBM).
 
 --op crc32 (default, the BASELINE metric) | fcs_verify (lnx_fcs_verify_batch,
 residue check of the same frames) | sum16 (lnx_sum16_batch: RFC 791 checksum of
-every frame as one segment, random pseudo-header seeds).
+every frame as one segment, random pseudo-header seeds) | ingress
+(lnx_ingress_verify_batch: the frames get Ethernet/IPv4/UDP headers written in
+place, so every frame takes the full header-sum + UDP-sum path).
 
 N=1 runs BASELINE configs[1] (1 M x 1500 B).  For N>1 (launched by
 torch.distributed.run, one rank per GPU) every rank owns its own contiguous
@@ -112,7 +114,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
-    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16"])
+    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
@@ -129,12 +131,20 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # LNETO_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box only): every rank
+    # uses cuda:0 and the timing collectives run over gloo instead of RCCL.
+    share = os.environ.get("LNETO_BENCH_SHARE_GPU") == "1"
+    gpu = 0 if share else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    cdev = torch.device("cpu") if share else dev  # device of the timing tensors
 
     wname, n_rank, flen, desc = workload_spec(args.workload, world)
     # Frame index slice of this rank within the global batch (weak scaling:
@@ -159,6 +169,15 @@ def main():
         d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
     elif args.op == "fcs_verify":
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    elif args.op == "ingress":
+        if flen is None or flen < 42:
+            raise SystemExit("--op ingress needs fixed-size frames of at least 42 bytes")
+        fr = d_bytes[: n_local * flen].view(n_local, flen)
+        hdr = bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0]) + (flen - 14).to_bytes(2, "big") \
+            + bytes.fromhex("12344000401100 00c0a80a01c0a80a02".replace(" ", "")) \
+            + bytes.fromhex("14e90035") + (flen - 34).to_bytes(2, "big")
+        fr[:, : len(hdr)] = torch.tensor(list(hdr), dtype=torch.uint8, device=dev)
+        d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -166,6 +185,8 @@ def main():
             L.sum16_batch(d_bytes, d_seg, d_len, d_seed, out=d_sum, stream=stream)
         elif args.op == "fcs_verify":
             L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+        elif args.op == "ingress":
+            L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         else:
             L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
 
@@ -190,13 +211,13 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max, kern_ms_max = float(t[0]), float(t[1])
     total_bytes = nbytes * world  # every rank owns the same byte count (fixed-size frames)
     if dist and flen is None:
-        tb = torch.tensor([nbytes], dtype=torch.float64, device=dev)
+        tb = torch.tensor([nbytes], dtype=torch.float64, device=cdev)
         dist.all_reduce(tb)
         total_bytes = int(tb.item())
 
@@ -207,6 +228,7 @@ def main():
         "crc32": "GiB/s CRC-32 over device-resident 1500B frames; % of HBM3E read peak",
         "fcs_verify": "GiB/s FCS verify (CRC-32 residue) over device-resident frames; % of HBM3E read peak",
         "sum16": "GiB/s RFC 791 internet checksum over device-resident segments; % of HBM3E read peak",
+        "ingress": "GiB/s receive-path checksum verdicts (IPv4 header + UDP) over device-resident frames",
     }[args.op]
     out = {
         "metric": metric,
@@ -239,7 +261,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
-                       "sum16": "lnx::sum16_segments_kernel"}[args.op],
+                       "sum16": "lnx::sum16_segments_kernel", "ingress": "lnx::ingress_verify_kernel"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "algorithmic_bytes_per_launch": nbytes,
         },
@@ -258,7 +280,7 @@ def main():
         if args.op == "sum16":
             got = d_sum.cpu().numpy().view(np.uint16)
             seeds = d_seed.cpu().numpy().view(np.uint32)
-        elif args.op == "fcs_verify":
+        elif args.op in ("fcs_verify", "ingress"):
             got = d_ok.cpu().numpy()
         else:
             got = d_crc.cpu().numpy().view(np.uint32)
@@ -269,6 +291,8 @@ def main():
                 want = O.payload_sum16(int(seeds[i]), fr)
             elif args.op == "fcs_verify":
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
+            elif args.op == "ingress":
+                want = O.ingress_verdict(fr)
             else:
                 want = O.crc32(fr)
             assert int(got[i]) == want, f"mismatch frame {i}"

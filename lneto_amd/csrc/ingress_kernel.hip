@@ -17,8 +17,10 @@
 // code the reference returns (errors.go:6-28).  Destination filtering and
 // handler lookup depend on stack configuration: taken as accept-all.
 //
-// Layout: one 16-lane row per frame, four frames per wave.  Header fields are
-// row-uniform byte loads (one request per row).  The sums use the identity of
+// Layout: one 16-lane row per frame, four frames per wave.  The row's first
+// batch of dword loads (frame offsets from 12 on) also carries every header
+// field: they are gathered from the row's lanes with ds_bpermute and realigned
+// with v_alignbyte, so a frame costs one round trip before its sums start.  The sums use the identity of
 // sum16_kernel.hip: the uint32 sum of big-endian 16-bit words of a segment that
 // starts at an even frame offset is 256*E + O (E / O = sums of the bytes at
 // even / odd frame offsets), and every segment here starts at an even offset
@@ -31,6 +33,7 @@
 namespace lnx {
 
 constexpr int kIngBlock = 256;
+constexpr int kIngUnroll = 8;  // dwords per lane in flight (512 B per row)
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
 constexpr uint32_t kVerifyEvilBit = 1;
@@ -69,8 +72,40 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const uint64_t len64 = e > s ? e - s : 0;
     const uint32_t L = len64 < 0x7FFFFFFFull ? (uint32_t)len64 : 0x7FFFFFFFu;
     const uint8_t* fr = bytes + s;
-    auto b8 = [&](uint32_t o) -> uint32_t { return o < L ? (uint32_t)fr[o] : 0u; };
-    auto be16 = [&](uint32_t o) -> uint32_t { return (b8(o) << 8) | b8(o + 1); };
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 3u);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(fr - mis);
+    // dword k of base holds frame offsets 4k - mis .. 4k - mis + 3
+    const int32_t kstart = (int32_t)((12 + mis) >> 2);          // dword holding frame offset 12
+    const int32_t kfend = (int32_t)((L + mis + 3) >> 2);         // dwords touching the frame
+
+    // ---- first batch: dwords kstart + p + 16u; it also holds every header field
+    uint32_t x[kIngUnroll];
+#pragma unroll
+    for (int u = 0; u < kIngUnroll; ++u) {
+      const int32_t k = kstart + (int32_t)p + 16 * u;
+      x[u] = L >= 14 && k < kfend ? base[k] : 0u;
+    }
+    // dword kstart + kk of this row (kk < 32) from the lane that loaded it
+    auto rowword = [&](int32_t kk) -> uint32_t {
+      const int addr = (int)((row * 16u + ((uint32_t)kk & 15u)) * 4u);
+      const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[0]);
+      const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[1]);
+      return kk < 16 ? a : b;
+    };
+    const uint32_t sh = (12 + mis) & 3u;  // byte of frame offset 12 inside dword kstart
+    const uint32_t w0 = rowword(0), w1 = rowword(1), w2 = rowword(2), w3 = rowword(3);
+    const uint32_t H0 = __builtin_amdgcn_alignbyte(w1, w0, sh);  // frame bytes 12..15
+    const uint32_t H1 = __builtin_amdgcn_alignbyte(w2, w1, sh);  // 16..19
+    const uint32_t H2 = __builtin_amdgcn_alignbyte(w3, w2, sh);  // 20..23
+    auto byt = [](uint32_t w, int i) -> uint32_t { return (w >> (8 * i)) & 0xFFu; };
+    auto be = [&](uint32_t w, int i) -> uint32_t { return (byt(w, i) << 8) | byt(w, i + 1); };
+    // big-endian 16-bit field at frame offset o (o + 1 < L, o >= 12)
+    auto field16 = [&](uint32_t o) -> uint32_t {
+      const int32_t kk = (int32_t)((o + mis) >> 2) - kstart;
+      const uint32_t lo = rowword(kk), hi = rowword(kk + 1);
+      const uint32_t v2 = __builtin_amdgcn_alignbyte(hi, lo, (o + mis) & 3u);
+      return ((v2 & 0xFFu) << 8) | ((v2 >> 8) & 0xFFu);
+    };
 
     // ---- header parse: row-uniform; v = verdict so far, sums requested below
     uint32_t v = 0;
@@ -80,7 +115,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     if (L < 14) {
       v = kErrTruncatedFrame;
     } else {
-      const uint32_t et = be16(12);
+      const uint32_t et = be(H0, 0);
       if (et <= 1500 && L < et) {
         v = kErrInvalidLengthField;
       } else if (et == 0x8100 && L < 18) {
@@ -90,15 +125,15 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
         if (M < 20) {
           v = kErrTruncatedFrame;
         } else {
-          const uint32_t b0 = b8(14), tl = be16(16), ihl = b0 & 15u;
+          const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
           if (tl < 20) v = kErrInvalidLengthField;
           else if (tl > M) v = kErrTruncatedFrame;
           else if (ihl < 5 || ihl * 4 > tl) v = kErrInvalidLengthField;
           else if ((b0 >> 4) != 4) v = kErrInvalidField;
-          else if ((flags & kVerifyEvilBit) && (be16(20) & (1u << 13))) v = kErrPacketDrop;
+          else if ((flags & kVerifyEvilBit) && (be(H2, 0) & (1u << 13))) v = kErrPacketDrop;
           if (v == 0) {
             hdr_sum = true;
-            const uint32_t hl = ihl * 4, proto = b8(23), P = tl - hl;
+            const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
             if (proto == 6) {
               l4_sum = true;
               pa = 26, pb = 34, la = 14 + hl, lb = 14 + tl;
@@ -107,7 +142,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               if (P < 8) {
                 v = kErrTruncatedFrame;
               } else {
-                const uint32_t ul = be16(14 + hl + 4);
+                const uint32_t ul = field16(14 + hl + 4);
                 if (ul < 8) v = kErrInvalidLengthField;
                 else if (ul > P) v = kErrTruncatedFrame;
                 else {
@@ -124,14 +159,14 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
         if (M < 40) {
           v = kErrTruncatedFrame;
         } else {
-          const uint32_t pl = be16(18), proto = b8(20);
+          const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
           if (pl + 40 > M) {
             v = kErrInvalidLengthField;
           } else if (proto == 6 || proto == 17) {
             if (proto == 17 && pl < 8) {
               v = kErrTruncatedFrame;
             } else {
-              const uint32_t ul = proto == 17 ? be16(58) : 8u;
+              const uint32_t ul = proto == 17 ? field16(58) : 8u;
               if (ul < 8) v = kErrInvalidLengthField;
               else if (ul > pl) v = kErrTruncatedFrame;
               else {
@@ -145,21 +180,28 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       }
     }
 
-    // ---- one pass over the aligned dwords covering [14, last byte summed)
+    // ---- the sums: the first batch is in x; later batches while the summed
+    // range [14, end) goes on (kIngUnroll dwords per lane in flight)
     uint32_t hE = 0, hO = 0, tE = 0, tO = 0;
-    if (hdr_sum || l4_sum) {
-      const int32_t end = l4_sum ? lb : 34;
-      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 3u);
-      const uint32_t* base = reinterpret_cast<const uint32_t*>(fr - mis);
-      const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;  // bytes at even frame offsets
-      const uint32_t wO = wE << 8 | wE >> 24;
-      const int32_t ha = hdr_sum ? 14 : 0, hb = hdr_sum ? 34 : 0;
-      // words whose bytes fall in [12, end): frame offset of word k's byte 0 is 4k - mis
-      for (int32_t k = (int32_t)((12 + mis) >> 2) + (int32_t)p; 4 * k - (int32_t)mis < end; k += 16) {
-        const int32_t o0 = 4 * k - (int32_t)mis;
-        const uint32_t x = base[k];
-        const uint32_t xh = x & range_mask(o0, ha, hb);
-        const uint32_t xt = x & (range_mask(o0, pa, pb) | range_mask(o0, la, lb));
+    const bool any_sum = hdr_sum || l4_sum;
+    const int32_t end = l4_sum ? lb : (hdr_sum ? 34 : 0);
+    const int32_t kend = any_sum ? (end + (int32_t)mis + 3) >> 2 : 0;
+    const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;  // bytes at even frame offsets
+    const uint32_t wO = wE << 8 | wE >> 24;
+    const int32_t ha = hdr_sum ? 14 : 0, hb = hdr_sum ? 34 : 0;
+    for (int32_t k0 = kstart + (int32_t)p; k0 < kend; k0 += 16 * kIngUnroll) {
+      if (k0 != kstart + (int32_t)p) {
+#pragma unroll
+        for (int u = 0; u < kIngUnroll; ++u) {
+          const int32_t k = k0 + 16 * u;
+          x[u] = k < kend ? base[k] : 0u;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kIngUnroll; ++u) {
+        const int32_t o0 = 4 * (k0 + 16 * u) - (int32_t)mis;
+        const uint32_t xh = x[u] & range_mask(o0, ha, hb);
+        const uint32_t xt = x[u] & (range_mask(o0, pa, pb) | range_mask(o0, la, lb));
         hE = __builtin_amdgcn_udot4(xh, wE, hE, false);
         hO = __builtin_amdgcn_udot4(xh, wO, hO, false);
         tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
@@ -178,7 +220,7 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   if (n == 0) return hipSuccess;
   const uint64_t frames_per_block = (kIngBlock / 64) * 4;
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
-  const uint64_t cap = (uint64_t)num_cus * 16;
+  const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL(ingress_verify_kernel, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n, flags,
                      verdict);

@@ -11,8 +11,9 @@
 // `<< 8` of crc.go:56.  Addition mod 2^32 is associative, so any lane/wave
 // split of the bytes gives the identical uint32 before the folds.
 //
-// One wave per segment; lane l reads aligned dwords l, l+64, ...; bytes outside
-// the segment are masked; v_dot4_u32_u8 forms the even/odd byte sums.
+// One 16-lane row per segment (four segments per wave); lane p reads aligned
+// dwords p, p+16, ... in batches; bytes outside the segment are masked;
+// v_dot4_u32_u8 forms the even/odd byte sums, DPP adds reduce the row.
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -21,51 +22,68 @@ namespace lnx {
 constexpr int kSumBlock = 256;
 constexpr int kSumWaves = kSumBlock / 64;
 
-__device__ __forceinline__ uint32_t wave_add(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);
-  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
-  return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) + __builtin_amdgcn_readlane((int)v, 16) +
-                    __builtin_amdgcn_readlane((int)v, 32) + __builtin_amdgcn_readlane((int)v, 48));
-}
-
 __device__ __forceinline__ uint16_t fold_sum16(uint32_t sum) {
   sum = (sum & 0xffffu) + (sum >> 16);
   return (uint16_t)~(uint16_t)(sum + (sum >> 16));
 }
 
+constexpr int kSumRowLanes = 16;  // one segment per 16-lane row, four per wave
+constexpr int kSumUnroll = 8;     // dwords per lane in flight per batch (512 B per row)
+
+__device__ __forceinline__ uint32_t sum_keep_from(int32_t lo) {
+  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+  return (uint32_t)(0xFFFFFFFFull << (8 * lo));
+}
+
+__device__ __forceinline__ uint32_t row_add16(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return v;
+}
+
+// One 16-lane row per segment: lane p reads aligned dwords p, p+16, ... of the
+// segment's aligned span, kSumUnroll at a time, masks the bytes outside the
+// segment and accumulates E and O with v_dot4_u32_u8.
 __global__ void __launch_bounds__(kSumBlock)
 sum16_segments_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                       const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
                       uint64_t nseg, uint16_t* __restrict__ out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t wave0 = (uint64_t)blockIdx.x * kSumWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
   const uint64_t nwaves = (uint64_t)gridDim.x * kSumWaves;
-  const uintptr_t base = reinterpret_cast<uintptr_t>(bytes);
-  for (uint64_t i = wave0; i < nseg; i += nwaves) {
-    const uint64_t s = off[i];
-    const uint64_t e = s + len[i];
-    const uint32_t mis = (uint32_t)((base + s) & 3u);
-    const uint64_t a0 = s - mis;                     // first aligned dword of the segment
-    const uint64_t nd = e > s ? (e - a0 + 3) >> 2 : 0;  // dwords touching [s, e)
-    // Even-offset bytes sit at dword byte positions {0,2} when the segment
-    // starts at an even address, {1,3} when it starts at an odd one.
-    const uint32_t even_w = (mis & 1u) ? 0x01000100u : 0x00010001u;
-    const uint32_t odd_w = (mis & 1u) ? 0x00010001u : 0x01000100u;
-    uint32_t acc = 0;
-    for (uint64_t k = lane; k < nd; k += 64) {
-      const uint64_t pos = a0 + 4 * k;
-      uint32_t w = *reinterpret_cast<const uint32_t*>(bytes + pos);
-      const int32_t lo = pos < s ? (int32_t)(s - pos) : 0;
-      const int32_t hi = (pos + 4 > e) ? (int32_t)(e - pos) : 4;
-      w &= (uint32_t)((0xFFFFFFFFull << (8 * lo)) & ~(0xFFFFFFFFull << (8 * hi)));
-      const uint32_t ev = __builtin_amdgcn_udot4(w, even_w, 0u, false);
-      const uint32_t od = __builtin_amdgcn_udot4(w, odd_w, 0u, false);
-      acc += (ev << 8) + od;
+  for (uint64_t q = (uint64_t)blockIdx.x * kSumWaves + (threadIdx.x >> 6); q * 4 < nseg; q += nwaves) {
+    const uint64_t i = q * 4 + row;
+    const bool live = i < nseg;
+    const uint64_t s = live ? off[i] : 0;
+    const uint32_t L = live ? len[i] : 0u;
+    const uint32_t sd = live && seed ? seed[i] : 0u;
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + s) & 3u);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(bytes + s - mis);
+    const uint32_t nw = L ? (mis + L + 3) >> 2 : 0u;  // dwords touching the segment
+    // bytes at even segment offsets sit at dword positions {0,2} when the
+    // segment starts 2-aligned, {1,3} otherwise
+    const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;
+    const uint32_t wO = (mis & 1u) ? 0x00010001u : 0x01000100u;
+    uint32_t E = 0, O = 0;
+    for (uint32_t k0 = p; k0 < nw; k0 += kSumRowLanes * kSumUnroll) {
+      uint32_t x[kSumUnroll];
+#pragma unroll
+      for (int u = 0; u < kSumUnroll; ++u) {
+        const uint32_t k = k0 + u * kSumRowLanes;
+        x[u] = k < nw ? base[k] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kSumUnroll; ++u) {
+        const int32_t o0 = (int32_t)(4 * (k0 + u * kSumRowLanes)) - (int32_t)mis;  // segment offset of byte 0
+        const uint32_t y = x[u] & sum_keep_from(-o0) & ~sum_keep_from((int32_t)L - o0);
+        E = __builtin_amdgcn_udot4(y, wE, E, false);
+        O = __builtin_amdgcn_udot4(y, wO, O, false);
+      }
     }
-    const uint32_t total = wave_add(acc) + (seed ? seed[i] : 0u);
-    if (lane == 0) out[i] = fold_sum16(total);
+    E = row_add16(E);
+    O = row_add16(O);
+    if (live && p == 0) out[i] = fold_sum16(sd + 256u * E + O);
   }
 }
 
@@ -73,8 +91,9 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
                                   const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                   hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  uint64_t grid = (n + kSumWaves - 1) / kSumWaves;
-  const uint64_t cap = (uint64_t)num_cus * 8;
+  const uint64_t seg_per_block = kSumWaves * 4;
+  uint64_t grid = (n + seg_per_block - 1) / seg_per_block;
+  const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL(sum16_segments_kernel, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
                      off, len, seed, n, out);
