@@ -105,6 +105,16 @@ int lnx_fcs_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t
 int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
                     const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream);
 
+/* Batched ethernet.CRC32Search (ethernet/crc.go:28-47), SURVEY.md §8(f).4:
+ * d_result[i] = CRC32Search(d_bytes[d_off[i] : d_off[i+1]], d_min_off[i]) —
+ * the first off >= max(minOff, 0) with CRC32(capture[:off]) ==
+ * LE32(capture[off:off+4]), or -1 (also when the capture is shorter than
+ * minOff + 4).  d_min_off may be NULL (all 0).  For PIO captures of unknown
+ * frame length (phy/rmii.md:265-271); every prefix CRC of a capture is
+ * computed in one parallel scan. */
+int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const int64_t* d_min_off, uint64_t n,
+                           int64_t* d_result, void* stream);
+
 /* Receive-path checksum verdicts, one fused kernel: for
  * every Ethernet frame d_bytes[d_off[i] : d_off[i+1]] (FCS already stripped)
  * d_verdict[i] = the result lneto's receive path reaches at its checksum

@@ -68,6 +68,7 @@ _sig = {
     "lnx_fcs_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_sum16_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_ingress_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
+    "lnx_crc32_search_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
@@ -199,6 +200,21 @@ def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
     if n > 0:
         _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
                                         _stream_ptr(stream)), "lnx_fcs_verify_batch")
+    return out
+
+
+def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
+    """ethernet.CRC32Search of every capture d_bytes[d_off[i]:d_off[i+1]] on the GPU
+    (lnx_crc32_search_batch).  d_min_off: int64 (N) or None.  Returns int64 (N), -1 = none."""
+    import torch
+    _dev_check(d_bytes, d_off, d_min_off)
+    n = d_off.numel() - 1
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int64, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_crc32_search_batch(d_bytes.data_ptr(), d_off.data_ptr(),
+                                          d_min_off.data_ptr() if d_min_off is not None else None, n,
+                                          out.data_ptr(), _stream_ptr(stream)), "lnx_crc32_search_batch")
     return out
 
 

@@ -13,12 +13,16 @@
 
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                               bool verify, const void* image, int num_cus, hipStream_t stream);
+                               bool verify, const void* image, int num_cus, hipStream_t stream, uint64_t* ctrs,
+                               uint32_t epoch);
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
+                                const void* image, int num_cus, hipStream_t stream, uint64_t* ctrs,
+                                uint32_t epoch, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream);
+hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
+                               const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream);
@@ -47,6 +51,17 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
   return img;
 }
 
+// Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
+// byte tables for k = 0..5 (search_kernel.hip).
+std::vector<uint32_t> build_search_tables() {
+  std::vector<uint32_t> t(256 + 6 * 1024);
+  for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
+  for (uint32_t k = 0; k < 6; ++k)
+    for (uint32_t m = 0; m < 4; ++m)
+      for (uint32_t e = 0; e < 256; ++e) t[256 + k * 1024 + m * 256 + e] = zshift_bytes(e << (8 * m), 4 << k);
+  return t;
+}
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -56,12 +71,44 @@ int hip_fail(hipError_t e, const char* what) {
   return LNX_EHIP;
 }
 
+// Chunk counters of the CRC kernel's stealing mode (crc32_kernel.hip): one
+// set of per-workgroup 64-bit counters per stream, tagged with a per-set epoch
+// that grows by one per launch.  Launches on one stream run in order, so a set
+// is never used by two launches at once; a stream beyond kCtrSets runs in
+// workgroup mode (no stealing) instead.
+constexpr int kCtrSets = 64;
+constexpr int kCtrPerSet = 1024;  // >= workgroups of a launch (one per CU)
+
 struct DeviceCtx {
   std::once_flag once;
   int status = LNX_OK;
   void* d_image = nullptr;
   int num_cus = 0;
+  uint64_t* d_ctrs = nullptr;
+  uint32_t* d_search = nullptr;  // crc32_search_kernel tables
+  std::mutex mu;
+  void* set_stream[kCtrSets] = {};
+  uint32_t set_epoch[kCtrSets] = {};
+  int sets_used = 0;
 };
+
+// Counter set and epoch for a launch on `stream` (nullptr / 0: workgroup mode).
+void ctr_set_for(DeviceCtx* c, void* stream, uint64_t** ctrs, uint32_t* epoch) {
+  *ctrs = nullptr;
+  *epoch = 0;
+  if (!c->d_ctrs) return;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int k = 0;
+  while (k < c->sets_used && c->set_stream[k] != stream) ++k;
+  if (k == c->sets_used) {
+    if (k == kCtrSets) return;
+    c->set_stream[k] = stream;
+    ++c->sets_used;
+  }
+  if (c->set_epoch[k] == 0xFFFFFFFFu) return;  // epoch space used up on this stream
+  *epoch = ++c->set_epoch[k];
+  *ctrs = c->d_ctrs + (size_t)k * kCtrPerSet;
+}
 
 constexpr int kMaxDevices = 64;
 DeviceCtx g_ctx[kMaxDevices];
@@ -92,6 +139,16 @@ int get_ctx(DeviceCtx** out) {
     if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(image)"); return; }
     err = hipMemcpy(c.d_image, img.data(), img.size() * 4, hipMemcpyHostToDevice);
     if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(image)"); return; }
+    const size_t ctr_bytes = sizeof(uint64_t) * kCtrSets * kCtrPerSet;
+    err = hipMalloc(reinterpret_cast<void**>(&c.d_ctrs), ctr_bytes);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(counters)"); return; }
+    err = hipMemset(c.d_ctrs, 0, ctr_bytes);  // epoch 0: stale for every launch
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemset(counters)"); return; }
+    const std::vector<uint32_t> st = build_search_tables();
+    err = hipMalloc(reinterpret_cast<void**>(&c.d_search), st.size() * 4);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(search tables)"); return; }
+    err = hipMemcpy(c.d_search, st.data(), st.size() * 4, hipMemcpyHostToDevice);
+    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(search tables)"); return; }
   });
   if (c.status != LNX_OK) return c.status;
   *out = &c;
@@ -105,8 +162,11 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
+  uint64_t* ctrs = nullptr;
+  uint32_t epoch = 0;
+  if (c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
   hipError_t e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
-                                     static_cast<hipStream_t>(stream));
+                                     static_cast<hipStream_t>(stream), ctrs, epoch);
   if (e != hipSuccess) return hip_fail(e, "crc32_frames_kernel launch");
   return LNX_OK;
 }
@@ -138,6 +198,19 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
   hipError_t e = launch_sum16_segments(d_bytes, d_off, d_len, d_seed, n, d_out, c->num_cus,
                                        static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "sum16_segments_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const int64_t* d_min_off, uint64_t n,
+                           int64_t* d_result, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_result) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_crc32_search(d_bytes, d_off, d_min_off, n, c->d_search, d_result, c->num_cus,
+                                     static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32_search_kernel launch");
   return LNX_OK;
 }
 
@@ -221,8 +294,11 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream), nullptr);
+  uint64_t* ctrs = nullptr;
+  uint32_t epoch = 0;
+  if (var < 100 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);  // var >= 100: workgroup mode
+  hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream), ctrs, epoch, nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
   return LNX_OK;
 }
@@ -237,8 +313,11 @@ int64_t lnx__crc32_timeline(int var, const uint8_t* d_bytes, const uint64_t* d_o
   if (st != LNX_OK) return st;
   if (!d_timeline) return (int64_t)crc32_launch_waves(n, c->num_cus);
   if (n == 0 || !d_bytes || !d_off || !d_crc) return LNX_EINVAL;
-  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream), d_timeline);
+  uint64_t* ctrs = nullptr;
+  uint32_t epoch = 0;
+  if (var < 100 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
+  hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream), ctrs, epoch, d_timeline);
   if (e != hipSuccess) return hip_fail(e, "crc32 timeline launch");
   return LNX_OK;
 }

@@ -43,6 +43,7 @@
 // low dword of off[nf+i]), shuffled to the rows with ds_bpermute.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 #include "lds_layout.hpp"
 
@@ -277,10 +278,27 @@ __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* byt
 // Workgroup-uniform context of the pipelined path.  Positions are
 // rel(x) = x - off[fb0] + adj, frame indices relative to fb0.
 struct WaveCtx {
-  uint32_t nfb, o0_lo, adj;  // frames of the workgroup, low dword of off[fb0], alignment
-  uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase)
-  __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc;
+  uint32_t nfb, o0_lo, adj;  // frames of the range, low dword of its first offset, alignment
+  uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase), workgroup mode
+  uint64_t* gctr;            // global chunk counter of the range (epoch << 32 | claimed), stealing mode
+  uint32_t gctr_off, epoch;  // byte offset of gctr in ctr_rsrc; this launch's epoch
+  __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc, ctr_rsrc;
 };
+
+// One returning 64-bit atomic add of v on the counter at byte voff, or (no
+// claim) a 64-bit load from an out-of-range offset: either way exactly one
+// vmcnt event, so the ring's count stays static.
+__device__ __forceinline__ void claim_or_nop(bool claim, bool leader, uint64_t& r, uint32_t voff, uint64_t v,
+                                             __amdgpu_buffer_rsrc_t rsrc) {
+  if (claim) {
+    if (leader) {  // one lane: a wave instruction with one active lane is still one vmcnt event
+      r = v;
+      asm volatile("s_nop 4\n\tbuffer_atomic_add_x2 %0, %1, %2, 0 offen sc0" : "+v"(r) : "v"(voff), "s"(rsrc));
+    }
+  } else {
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(r) : "v"(kOOB), "s"(rsrc));
+  }
+}
 
 // RL: lanes per row, KS: window steps per item, S: ring slots, CH: frames per
 // chunk, VAR: profiling knob (0 = product, 1 = loads +
@@ -294,7 +312,7 @@ struct WaveCtx {
 // sees its chunks as one virtual frame sequence v = 0, 1, ...: it holds the
 // bases of the chunk v is in (bc) and of the next one (bn), which covers the
 // S*NR-frame bounds window every slot prefetches.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR>
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool STEAL>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
@@ -302,21 +320,35 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   static_assert(RL == 4 || RL == 16, "row width");
   static_assert(S >= 2 && S * NR <= (uint32_t)CH && CH <= 64, "bounds window within two chunks");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
-  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3;  // per slot: steps, junk word, frame start + end
+  // a claim issued at one chunk boundary has landed (S slots later) before the next
+  static_assert(!STEAL || (uint32_t)CH >= (S + 1) * NR, "claim latency");
+  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3 + (STEAL ? 1 : 0);  // steps, junk, start + end, claim
   constexpr int kPending = (S - 1) * kLoads;       // loads issued after a slot's own
   const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bf = L.bf, bt = L.bt;
   const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
   const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
 
   // ---- chunks (uniform)
-  auto claim = [&]() -> uint32_t {
+  // a claimed count of another epoch (cannot happen after the range's epoch
+  // init) is treated as exhausted
+  auto count_of = [&](uint64_t old) -> uint32_t {
+    return (uint32_t)(old >> 32) == cx.epoch ? (uint32_t)old : nfb;
+  };
+  auto claim = [&]() -> uint32_t {  // synchronous: outside the ring only, or in workgroup mode
     uint32_t b = 0;
-    if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, (uint32_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if constexpr (STEAL) {
+      if (lane == 0) b = count_of(__hip_atomic_fetch_add(cx.gctr, (uint64_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    } else {
+      if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, (uint32_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
   uint32_t cc = 0;          // virtual chunk index of bc
   uint32_t bc = claim();    // first frame of chunk cc
   uint32_t bn = claim();    // first frame of chunk cc + 1
+  uint32_t bnn = STEAL ? claim() : 0u;  // stealing mode: chunk cc + 2, claimed ahead asynchronously
+  int pend = -1;            // slot whose claim is in flight (stealing mode)
+  uint64_t cl[S];           // per-slot claim result registers
   auto vframe = [&](uint32_t v) -> uint32_t {  // frame of virtual index v, kNoFrame past the work
     const uint32_t c0 = cc * CH;
     const uint32_t f = v < c0 + CH ? bc + (v - c0) : (v < c0 + 2 * CH ? bn + (v - c0 - CH) : kNoFrame);
@@ -342,6 +374,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 #pragma unroll
     for (int k = 0; k < KS; ++k) w[s][k] = 0;
     jk[s] = 0;
+    cl[s] = 0;
     it_f[s] = kNoFrame;
     it_n[s] = it_t[s] = it_j0[s] = it_ns[s] = 0;
     hw[s] = false;
@@ -413,10 +446,20 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }
     jk[s] = ld_buf<0>(jv, data_rsrc);
     // 4. bounds of the next S*NR frames, for this slot's next issue
+    bool claim_now = false;
     if (nf >= (cc + 1) * CH) {  // at most one chunk boundary per issue (cnt <= NR <= CH)
       ++cc;
       bc = bn;
-      bn = claim();
+      if constexpr (STEAL) {
+        bn = bnn;  // landed: claimed at the previous boundary, >= S slots ago
+        claim_now = true;
+      } else {
+        bn = claim();
+      }
+    }
+    if constexpr (STEAL) {
+      claim_or_nop(claim_now, lane == 0, cl[s], cx.gctr_off, (uint64_t)CH, cx.ctr_rsrc);
+      if (claim_now) pend = s;
     }
     const uint32_t g = vframe(nf + lane);
     const uint32_t go = g != kNoFrame ? g * 8u : kOOB;
@@ -429,6 +472,13 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   auto compute = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     slot_wait<kPending, KS>(w[s], jk[s], sb[s], eb[s]);
+    if constexpr (STEAL) {
+      asm volatile("" : "+v"(cl[s]));
+      if (pend == s) {
+        bnn = (uint32_t)__builtin_amdgcn_readfirstlane((int)count_of(cl[s]));
+        pend = -1;
+      }
+    }
     const uint32_t n = it_n[s], t = it_t[s], ns = it_ns[s], j0 = it_j0[s];
     const uint32_t J = n ? (n + t + SB - 1) >> kSbLog : 0u;
     const bool alive = it_f[s] != kNoFrame;
@@ -521,7 +571,7 @@ template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 2, in
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
-                  uint64_t* __restrict__ timeline) {
+                  uint64_t* __restrict__ ctrs, uint32_t epoch, uint64_t* __restrict__ timeline) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path
@@ -559,12 +609,61 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   }
   if (fb1 == fb0) return;
 
-  // The workgroup's byte range, addressed through one buffer descriptor whose
-  // base is 4-byte aligned: rel(x) = x - off[fb0] + adj.
-  const uint64_t range = ob1 > ob0 ? ob1 - ob0 : 0;  // non-decreasing offsets are the contract
-  const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + ob0) & 3u);
-  if (range + adj + 4096 >= (1ull << 31)) {
-    // gigabyte frames: static per-wave ranges on the unpipelined path
+  // A range (a workgroup's slice of frames) is addressed through one buffer
+  // descriptor whose base is 4-byte aligned: rel(x) = x - off[fb0] + adj.
+  struct Range {
+    uint64_t f0, f1, o0, o1;
+    bool fits;  // byte range within 31-bit buffer offsets
+  };
+  auto range_of = [&](uint64_t b, uint64_t o0, uint64_t o1) -> Range {
+    Range r;
+    r.f0 = b * per_block < nframes ? b * per_block : nframes;
+    r.f1 = r.f0 + per_block < nframes ? r.f0 + per_block : nframes;
+    r.o0 = o0, r.o1 = o1;
+    const uint64_t bytes_ = o1 > o0 ? o1 - o0 : 0;  // non-decreasing offsets are the contract
+    const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + o0) & 3u);
+    r.fits = bytes_ + adj + 4096 < (1ull << 31);
+    return r;
+  };
+  auto ctx_of = [&](const Range& r) -> WaveCtx {
+    WaveCtx cx;
+    const uint64_t bytes_ = r.o1 > r.o0 ? r.o1 - r.o0 : 0;
+    cx.adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + r.o0) & 3u);
+    cx.nfb = (uint32_t)(r.f1 - r.f0);
+    cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + r.o0 - cx.adj), (short)0,
+                                                     (int)((bytes_ + cx.adj + 3) & ~3ull), 0x00020000);
+    cx.off_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(off + r.f0), (short)0,
+                                                    (int)((cx.nfb + 1) * 8u), 0x00020000);
+    constexpr uint32_t elem = MODE == CrcMode::kCrc ? 4u : 1u;
+    cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + r.f0 * elem, (short)0,
+                                                    (int)(cx.nfb * elem), 0x00020000);
+    cx.ctr_rsrc = __builtin_amdgcn_make_buffer_rsrc(ctrs, (short)0, (int)(gridDim.x * 8u), 0x00020000);
+    cx.o0_lo = (uint32_t)r.o0;
+    cx.ctr = lds_words + kCtrBase / 4;
+    cx.gctr = nullptr;
+    cx.gctr_off = 0;
+    cx.epoch = epoch;
+    return cx;
+  };
+  auto run = [&](const WaveCtx& cx, auto steal) {
+    constexpr bool kSteal = decltype(steal)::value;
+    asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
+    if (narrow) {
+      L.p = lane & 3u, L.row = lane >> 2;
+      rows_body<MODE, 4, KS4, S4, CH4, VAR, kSteal>(lds, L, cx);
+    } else {
+      L.p = lane & 15u, L.row = lane >> 4;
+      rows_body<MODE, 16, KS16, S16, CH16, VAR, kSteal>(lds, L, cx);
+    }
+  };
+
+  const Range own = range_of(blockIdx.x, ob0, ob1);
+  if (!own.fits) {
+    // gigabyte frames: static per-wave ranges on the unpipelined path; thieves
+    // are told this slice is taken
+    if (ctrs && lane == 0)
+      __hip_atomic_fetch_max(ctrs + blockIdx.x, ((uint64_t)epoch << 32) | 0xFFFFFFFFull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow) {
@@ -577,31 +676,55 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
     return;
   }
-  WaveCtx cx;
-  cx.nfb = (uint32_t)(fb1 - fb0);
-  cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + ob0 - adj), (short)0,
-                                                   (int)((range + adj + 3) & ~3ull), 0x00020000);
-  cx.off_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(off + fb0), (short)0,
-                                                  (int)((cx.nfb + 1) * 8u), 0x00020000);
-  constexpr uint32_t elem = MODE == CrcMode::kCrc ? 4u : 1u;
-  cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + fb0 * elem, (short)0,
-                                                  (int)(cx.nfb * elem), 0x00020000);
-  cx.o0_lo = (uint32_t)ob0;
-  cx.adj = adj;
-  cx.ctr = lds_words + kCtrBase / 4;
-  asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
-  if (narrow) {
-    L.p = lane & 3u, L.row = lane >> 2;
-    rows_body<MODE, 4, KS4, S4, CH4, VAR>(lds, L, cx);
+  if (!ctrs) {
+    // workgroup mode: chunks of the own slice from the LDS counter
+    run(ctx_of(own), std::false_type{});
   } else {
-    L.p = lane & 15u, L.row = lane >> 4;
-    rows_body<MODE, 16, KS16, S16, CH16, VAR>(lds, L, cx);
+    // stealing mode: chunks of the own slice from its global counter, then of
+    // the slice with the most frames left, until none has 2 chunks left
+    constexpr uint32_t kMinSteal = 2 * (uint32_t)(CH16 > CH4 ? CH16 : CH4);
+    uint64_t b = blockIdx.x;
+    Range r = own;
+    for (;;) {
+      WaveCtx cx = ctx_of(r);
+      cx.gctr = ctrs + b;
+      cx.gctr_off = (uint32_t)b * 8u;
+      uint64_t seen = 0;  // epoch init: a stale count (older epoch) becomes (epoch, 0)
+      if (lane == 0) seen = __hip_atomic_fetch_max(cx.gctr, (uint64_t)epoch << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("" ::"v"(seen));
+      run(cx, std::true_type{});
+      // the slice with the most frames left (lane-parallel scan of the counters)
+      uint64_t best = 0;
+      for (uint32_t w = lane; w < gridDim.x; w += 64) {
+        const uint64_t f0 = (uint64_t)w * per_block < nframes ? (uint64_t)w * per_block : nframes;
+        const uint64_t f1 = f0 + per_block < nframes ? f0 + per_block : nframes;
+        const uint64_t c = __hip_atomic_load(ctrs + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t claimed = (uint32_t)(c >> 32) == epoch ? (uint32_t)c : 0u;
+        const uint64_t left = claimed < f1 - f0 ? f1 - f0 - claimed : 0u;
+        const uint64_t key = (left << 32) | w;
+        best = key > best ? key : best;
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)best, m, 64);
+        best = o > best ? o : best;
+      }
+      best = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(best >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)best);
+      if ((best >> 32) < kMinSteal) break;
+      b = (uint32_t)best;
+      const uint64_t f0 = b * per_block < nframes ? b * per_block : nframes;
+      const uint64_t f1 = f0 + per_block < nframes ? f0 + per_block : nframes;
+      r = range_of(b, off[f0], off[f1]);
+      if (!r.fits) break;  // (marked taken by its owner; cannot happen for a slice with frames left)
+    }
   }
   if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                       const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr) {
+                       const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs, uint32_t epoch,
+                       uint64_t* timeline = nullptr) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
   uint64_t grid = (n + per_block - 1) / per_block;
@@ -611,7 +734,8 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const uint4* img = static_cast<const uint4*>(images);
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
-  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, timeline)
+  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, ctrs, \
+                     epoch, timeline)
   if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
@@ -621,7 +745,7 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;              // lookups + bookkeeping only
       case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3); break;
-      case 28: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 8); break;   // 8-frame chunks
+      case 28: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 12); break;  // 12-frame chunks
       case 29: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 32); break;  // 32-frame chunks
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 8, 3); break;  // forced 4-lane rows
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 16, 3); break;
@@ -638,12 +762,14 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
 
 // Host-side launch helpers (called from api.cpp).
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                               const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream);
+                               const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs,
+                               uint32_t epoch) {
+  return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream, ctrs, epoch);
 }
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
-  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, timeline);
+                                const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs,
+                                uint32_t epoch, uint64_t* timeline) {
+  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, ctrs, epoch, timeline);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

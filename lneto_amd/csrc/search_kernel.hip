@@ -1,0 +1,107 @@
+// search_kernel.hip — batched ethernet.CRC32Search, gfx950.
+//
+// Reference: ethernet.CRC32Search(data, minOffCRC) (lneto ethernet/crc.go:28-47)
+// returns the first off in [max(minOff, 0), len-4] with
+//     CRC32(data[:off]) == LE32(data[off:off+4])
+// or -1 (also when len < minOff + 4).  The Go code extends the CRC one byte at a
+// time; here every prefix state of a capture is computed at once.  The test is
+// the residue form of the same equality: CRC32(M || LE32(CRC32(M))) is the
+// constant 0x2144DF1C for every M, and the 4-byte step is a bijection of the
+// register, so the equality holds exactly when the register after data[:off+4]
+// is ~0x2144DF1C = 0xDEBB20E3.
+//
+// One wave per capture, 256 bytes per block: lane j takes word j of the block;
+// the carried register (0xFFFFFFFF at the start: the CRC init) is XOR-ed into
+// word 0, so with init 0
+//   a_j = Z_4(w_j)                       (register contribution of word j)
+//   inclusive scan over j with (A, B) -> Z_{|B|}(A) ^ B, |B| = 4*2^k bytes
+// gives the register after every word; four byte steps from the state before
+// the word give the register after every byte.  Z_{4*2^k} (k = 0..5) are byte
+// tables in LDS (shared; lookups here are rare next to the frame CRC path).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lnx {
+
+constexpr int kSearchBlock = 256;
+constexpr uint32_t kSearchTabBytes = 1024 + 6 * 4096;  // byte-step table + 6 x 4 byte tables
+constexpr uint32_t kResidueRegister = 0xDEBB20E3u;     // ~0x2144DF1C
+
+// Z_{4*2^k}(x) through the four byte tables of level k
+__device__ __forceinline__ uint32_t zlevel(const uint32_t* lds, int k, uint32_t x) {
+  const uint32_t* z = lds + 256 + k * 1024;
+  return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
+}
+
+__global__ void __launch_bounds__(kSearchBlock)
+crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                    const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                    int64_t* __restrict__ result) {
+  __shared__ uint32_t lds[kSearchTabBytes / 4];
+  for (uint32_t i = threadIdx.x; i < kSearchTabBytes / 4; i += kSearchBlock) lds[i] = tables[i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kSearchBlock / 64);
+  for (uint64_t c = (uint64_t)blockIdx.x * (kSearchBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
+    const uint64_t s = off[c], e = off[c + 1];
+    const int64_t L = e > s ? (int64_t)(e - s) : 0;
+    int64_t m = min_off ? min_off[c] : 0;
+    if (m < 0) m = 0;
+    int64_t found = -1;
+    if (L >= m + 4) {
+      const uint8_t* d = bytes + s;
+      uint32_t carry = 0xFFFFFFFFu;  // register entering the block (CRC init)
+      // only blocks that can hold a state index k in [m + 4, L] matter, but the
+      // register has to be carried from the start
+      for (int64_t B = 0; B < L && found < 0; B += 256) {
+        const int64_t base = B + 4 * (int64_t)lane;
+        uint32_t w = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w |= (base + q < L ? (uint32_t)d[base + q] : 0u) << (8 * q);
+        if (lane == 0) w ^= carry;
+        // inclusive scan of the word registers
+        uint32_t a = zlevel(lds, 0, w);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const uint32_t dd = 1u << k;
+          // a holds the words (lane - 2^k, lane]; the partial ending at lane - 2^k
+          // is advanced over those 4*2^k bytes and folded in
+          const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)a);
+          a ^= lane >= dd ? zlevel(lds, k, prev) : 0u;
+        }
+        // register before this lane's word, then per-byte states
+        uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)a);
+        r = lane == 0 ? 0u : r;
+        int64_t best = -1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          r = lds[(r ^ (w >> (8 * q))) & 0xFFu] ^ (r >> 8);
+          const int64_t k = base + q + 1;  // bytes consumed
+          if (best < 0 && r == kResidueRegister && k >= m + 4 && k <= L) best = k - 4;
+        }
+        // first hit of the wave: lanes are in byte order, and within a lane q is
+        const uint64_t hits = __builtin_amdgcn_ballot_w64(best >= 0);
+        if (hits) {
+          const uint32_t first = (uint32_t)__builtin_ctzll(hits);
+          found = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, first)) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)best >> 32), first) << 32));
+        }
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
+      }
+    }
+    if (lane == 0) result[c] = found;
+  }
+}
+
+hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
+                               const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t grid = (n + 3) / 4;
+  const uint64_t cap = (uint64_t)num_cus * 8;
+  if (grid > cap) grid = cap;
+  hipLaunchKernelGGL(crc32_search_kernel, dim3((unsigned)grid), dim3(kSearchBlock), 0, stream, bytes, off, min_off,
+                     n, tables, result);
+  return hipGetLastError();
+}
+
+}  // namespace lnx

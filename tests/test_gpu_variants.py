@@ -17,9 +17,10 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# 20/21: 16-lane rows (KS, S) = (24, 2), (12, 3); 28/29: (24, 2) with 8 / 32-frame chunks;
+# 20/21: 16-lane rows (KS, S) = (24, 2), (12, 3); 28/29: (24, 2) with 12 / 32-frame chunks;
+# every id + 100: the same in workgroup mode (no global counters, no stealing)
 # 22..25: 4-lane rows (8,3), (16,3), (12,2), (6,3)
-FORCED = [20, 21, 22, 23, 24, 25, 28, 29]
+FORCED = [20, 21, 22, 23, 24, 25, 28, 29, 120, 122]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

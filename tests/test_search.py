@@ -1,0 +1,55 @@
+"""Batched ethernet.CRC32Search (ethernet/crc.go:28-47), SURVEY.md §8(f).4:
+lnx_crc32_search_batch against the golden cases (ethernet/crc_test.go shapes)
+and the Go-semantics oracle on random captures with embedded FCS."""
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cuda, caps, mins):
+    import torch
+    import lneto_amd as L
+    offs = np.zeros(len(caps) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(c) for c in caps])
+    data = np.frombuffer(b"".join(caps) + b"\0" * 8, dtype=np.uint8).copy()
+    d = torch.from_numpy(data).to(cuda)
+    o = torch.from_numpy(offs).to(cuda)
+    m = torch.tensor(mins, dtype=torch.int64, device=cuda)
+    return L.crc32_search_batch(d, o, m).cpu().numpy().tolist()
+
+
+def test_golden_search_cases(cuda, golden):
+    cases = golden["crc32_search_cases"]
+    got = _run(cuda, [bytes.fromhex(c["data"]) for c in cases], [c["min_off"] for c in cases])
+    assert got == [c["want"] for c in cases]
+
+
+def test_random_captures(cuda):
+    rng = np.random.default_rng(21)
+    caps, mins = [], []
+    for i in range(3000):
+        kind = i % 6
+        n = int(rng.integers(0, 2100))
+        body = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        if kind in (0, 1, 2):  # a frame with its FCS, then trailing capture garbage
+            cut = int(rng.integers(0, n + 1))
+            cap = body[:cut] + struct.pack("<I", O.crc32(body[:cut])) + body[cut:cut + int(rng.integers(0, 64))]
+        elif kind == 3:        # two valid FCS positions: the first one wins
+            a = body[: n // 3]
+            f1 = a + struct.pack("<I", O.crc32(a))
+            cap = f1 + struct.pack("<I", O.crc32(f1)) + body[:10]
+        elif kind == 4:        # leading zeros: off 0 matches CRC32(nil) == 0
+            cap = b"\0\0\0\0" + body[:200]
+        else:                  # no FCS anywhere (almost surely)
+            cap = body
+        caps.append(cap)
+        mins.append(int(rng.choice([0, -5, 1, 3, len(cap) // 2, len(cap) - 4, len(cap) - 3, len(cap) + 10])))
+    got = _run(cuda, caps, mins)
+    want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]

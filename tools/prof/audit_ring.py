@@ -23,6 +23,18 @@ def regs(text):
     return out
 
 
+def vmem_dest(t):
+    """(is a vmcnt event, destination registers) of an instruction.  On gfx9
+    loads, returning atomics (sc0) and stores all count in vmcnt."""
+    if t.startswith("buffer_load_dword") or (t.startswith("global_load_dword ") and t.endswith(" nt")):
+        return True, regs(t.split(",")[0].split(None, 1)[1])
+    if t.startswith("buffer_atomic_") and " sc0" in t:
+        return True, regs(t.split(",")[0].split(None, 1)[1])
+    if t.startswith("buffer_store") or t.startswith("global_store"):
+        return True, set()
+    return False, set()
+
+
 def main():
     path, sym = sys.argv[1], sys.argv[2]
     lines = open(path).read().split("\n")
@@ -31,8 +43,9 @@ def main():
     body = [l.split(";")[0].strip() for l in lines[start:end + 1]]
     ring, first = set(), None
     for i, t in enumerate(body):
-        if t.startswith("buffer_load_dword ") or (t.startswith("global_load_dword ") and t.endswith(" nt")):
-            ring |= regs(t.split(",")[0])
+        ev, d = vmem_dest(t)
+        if ev and d:
+            ring |= d
             first = i if first is None else first
     bad = []
     # linear-order pending check: vmcnt(N) retires all but the N youngest loads
@@ -41,12 +54,13 @@ def main():
         if t.startswith("s_waitcnt") and "vmcnt(" in t:
             n = int(re.search(r"vmcnt\((\d+)\)", t).group(1))
             seq = seq[-n:] if n else []
-            pending = {r for r in pending if r in seq}
+            live = set().union(*seq) if seq else set()
+            pending = {r for r in pending if r in live}
             continue
-        if t.startswith("buffer_load_dword ") or (t.startswith("global_load_dword ") and t.endswith(" nt")):
-            d = t.split(",")[0].split()[1]
-            pending.add(d)
-            seq.append(d)
+        ev, d = vmem_dest(t)
+        if ev:
+            pending |= d
+            seq.append(frozenset(d))
             continue
         if not t or t.startswith("."):
             continue
@@ -57,7 +71,7 @@ def main():
     # descriptor; hipcc pads only instructions it can see, so every asm buffer
     # load must be preceded by an s_nop >= 4 (or >= 5 other instructions).
     for i, t in enumerate(body):
-        if not t.startswith("buffer_load_dword "):
+        if not (t.startswith("buffer_load_dword") or t.startswith("buffer_atomic_")):
             continue
         rs = regs(t.split(",")[2]) if len(t.split(",")) > 2 else set()
         waits = 0
