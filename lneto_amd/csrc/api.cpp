@@ -162,9 +162,11 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
+  // Workgroup mode: in stealing mode the in-order vmcnt makes every slot wait
+  // behind the chunk claim's device-scope atomic, which cost 12 % at 1500 B
+  // (DESIGN.md §3.1); the stealing path stays reachable as variants 200+.
   uint64_t* ctrs = nullptr;
   uint32_t epoch = 0;
-  if (c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
   hipError_t e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
                                      static_cast<hipStream_t>(stream), ctrs, epoch);
   if (e != hipSuccess) return hip_fail(e, "crc32_frames_kernel launch");
@@ -296,7 +298,7 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   if (st != LNX_OK) return st;
   uint64_t* ctrs = nullptr;
   uint32_t epoch = 0;
-  if (var < 100 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);  // var >= 100: workgroup mode
+  if (var >= 200 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);  // 200+: stealing mode
   hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                       static_cast<hipStream_t>(stream), ctrs, epoch, nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
@@ -315,7 +317,7 @@ int64_t lnx__crc32_timeline(int var, const uint8_t* d_bytes, const uint64_t* d_o
   if (n == 0 || !d_bytes || !d_off || !d_crc) return LNX_EINVAL;
   uint64_t* ctrs = nullptr;
   uint32_t epoch = 0;
-  if (var < 100 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
+  if (var >= 200 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
   hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                       static_cast<hipStream_t>(stream), ctrs, epoch, d_timeline);
   if (e != hipSuccess) return hip_fail(e, "crc32 timeline launch");

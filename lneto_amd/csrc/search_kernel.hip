@@ -12,7 +12,8 @@
 //
 // One wave per capture, 256 bytes per block: lane j takes word j of the block;
 // the carried register (0xFFFFFFFF at the start: the CRC init) is XOR-ed into
-// word 0, so with init 0
+// word 0 for the scan (exact after whole words; the byte states inside word 0
+// start from the carry itself), so with init 0
 //   a_j = Z_4(w_j)                       (register contribution of word j)
 //   inclusive scan over j with (A, B) -> Z_{|B|}(A) ^ B, |B| = 4*2^k bytes
 // gives the register after every word; four byte steps from the state before
@@ -58,9 +59,9 @@ crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restric
         uint32_t w = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) w |= (base + q < L ? (uint32_t)d[base + q] : 0u) << (8 * q);
-        if (lane == 0) w ^= carry;
-        // inclusive scan of the word registers
-        uint32_t a = zlevel(lds, 0, w);
+        // inclusive scan of the word registers (carry folded into word 0: exact
+        // after whole words only)
+        uint32_t a = zlevel(lds, 0, lane == 0 ? w ^ carry : w);
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           const uint32_t dd = 1u << k;
@@ -69,9 +70,10 @@ crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restric
           const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)a);
           a ^= lane >= dd ? zlevel(lds, k, prev) : 0u;
         }
-        // register before this lane's word, then per-byte states
+        // register before this lane's word (the carry itself for word 0), then
+        // per-byte states over the unmodified bytes
         uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)a);
-        r = lane == 0 ? 0u : r;
+        r = lane == 0 ? carry : r;
         int64_t best = -1;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
