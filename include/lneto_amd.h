@@ -89,6 +89,24 @@ uint16_t lnx_never_zero_sum(uint16_t sum16);
 int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n,
                     uint32_t* d_crc, void* stream);
 
+/* Segment form of lnx_crc32_batch for frames that are not packed back to back
+ * (ring slots): d_crc[i] = CRC32(d_bytes[d_start[i] : d_start[i] + d_len[i]]).
+ * Frames must be in increasing address order and must not overlap. */
+int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
+                       uint32_t* d_crc, void* stream);
+
+/* Batched TX FCS append: the tail of
+ * StackEthernet.Encapsulate with the CRC32Update hook set
+ * (internet/stack-ethernet.go:200-214) for every frame
+ * d_bytes[d_start[i] : d_start[i] + d_len[i]]: zero-pad to 60 bytes, write
+ * LE32(CRC32(padded frame)) after it, d_len[i] = padded length + 4.  Each frame
+ * may grow to `capacity` bytes; a frame that would not fit is left untouched
+ * with d_status[i] = 6 (lneto.ErrShortBuffer), else d_status[i] = 0.  Frames in
+ * increasing address order, at least `capacity` bytes apart.  The reference's
+ * onSend hook (between padding and FCS) has no batch equivalent. */
+int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
+                         uint8_t* d_status, void* stream);
+
 /* FCS verify of received frames that still carry their 4-byte LE FCS:
  * d_ok[i] = 1 iff len_i >= 4 and CRC32(f[:len_i-4]) == LE32(f[len_i-4:]),
  * evaluated as the residue test CRC32(f) == LNX_CRC32_RESIDUE.  This is the

@@ -69,6 +69,8 @@ _sig = {
     "lnx_sum16_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_ingress_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
     "lnx_crc32_search_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_crc32_segments": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "lnx_fcs_append_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
     "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
@@ -201,6 +203,34 @@ def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
         _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
                                         _stream_ptr(stream)), "lnx_fcs_verify_batch")
     return out
+
+
+def crc32_segments(d_bytes, d_start, d_len, out=None, stream=None):
+    """CRC32 of every frame d_bytes[d_start[i] : d_start[i] + d_len[i]] (lnx_crc32_segments);
+    d_start int64, d_len int32; frames in address order, not overlapping."""
+    import torch
+    _dev_check(d_bytes, d_start, d_len)
+    n = d_start.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_crc32_segments(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n,
+                                      out.data_ptr(), _stream_ptr(stream)), "lnx_crc32_segments")
+    return out
+
+
+def fcs_append_batch(d_bytes, d_start, d_len, capacity: int, status=None, stream=None):
+    """TX FCS append in place (lnx_fcs_append_batch): pad to 60, append LE FCS,
+    d_len (int32, updated) += padding + 4.  Returns the uint8 status (0 or 6)."""
+    import torch
+    _dev_check(d_bytes, d_start, d_len)
+    n = d_start.numel()
+    if status is None:
+        status = torch.empty(n, dtype=torch.uint8, device=d_bytes.device)
+    if n > 0:
+        _check(lib.lnx_fcs_append_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n, capacity,
+                                        status.data_ptr(), _stream_ptr(stream)), "lnx_fcs_append_batch")
+    return status
 
 
 def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):

@@ -23,6 +23,11 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
                                  uint8_t* verdict, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream);
+hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                                 void* out, const void* images, int num_cus, hipStream_t stream);
+hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                             uint8_t* status, uint32_t* crc_scratch, const void* images, int num_cus,
+                             hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream);
@@ -200,6 +205,37 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
   hipError_t e = launch_sum16_segments(d_bytes, d_off, d_len, d_seed, n, d_out, c->num_cus,
                                        static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "sum16_segments_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
+                       uint32_t* d_crc, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_start || !d_len || !d_crc) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_crc32_segments(d_bytes, d_start, d_len, n, d_crc, c->d_image, c->num_cus,
+                                       static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel (segments) launch");
+  return LNX_OK;
+}
+
+int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
+                         uint8_t* d_status, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_start || !d_len || !d_status) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* crc = nullptr;  // stream-ordered scratch for the CRCs
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&crc), n * 4, s);
+  if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(fcs scratch)");
+  e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, crc, c->d_image, c->num_cus, s);
+  const hipError_t f = hipFreeAsync(crc, s);
+  if (e != hipSuccess) return hip_fail(e, "fcs append launch");
+  if (f != hipSuccess) return hip_fail(f, "hipFreeAsync(fcs scratch)");
   return LNX_OK;
 }
 

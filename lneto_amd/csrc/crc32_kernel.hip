@@ -239,12 +239,12 @@ struct Lanes {
 // byte loads with explicit bounds, no pipelining.
 template <CrcMode MODE, int RL>
 __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* bytes, const uint64_t* off,
-                             uint64_t fw0, uint64_t fw1, void* out) {
+                             const uint32_t* seg_len, uint64_t fw0, uint64_t fw1, void* out) {
   constexpr uint32_t NR = 64 / RL, SB = 4 * RL;
   const uint64_t fend = fw0 + ((fw1 - fw0 + NR - 1) / NR) * NR;
   for (uint64_t f = fw0 + L.row; f < fend; f += NR) {
     const bool live = f < fw1;
-    const uint64_t s = live ? off[f] : 0, e = live ? off[f + 1] : 0;
+    const uint64_t s = live ? off[f] : 0, e = live ? (seg_len ? s + seg_len[f] : off[f + 1]) : 0;
     const uint64_t n = e > s ? e - s : 0;
     const uint64_t J = (n + SB - 1) / SB;
     uint32_t reg = 0;
@@ -283,6 +283,7 @@ struct WaveCtx {
   uint64_t* gctr;            // global chunk counter of the range (epoch << 32 | claimed), stealing mode
   uint32_t gctr_off, epoch;  // byte offset of gctr in ctr_rsrc; this launch's epoch
   __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc, ctr_rsrc;
+  __amdgpu_buffer_rsrc_t len_rsrc;  // segment mode: the length array
 };
 
 // One returning 64-bit atomic add of v on the counter at byte voff, or (no
@@ -312,7 +313,7 @@ __device__ __forceinline__ void claim_or_nop(bool claim, bool leader, uint64_t& 
 // sees its chunks as one virtual frame sequence v = 0, 1, ...: it holds the
 // bases of the chunk v is in (bc) and of the next one (bn), which covers the
 // S*NR-frame bounds window every slot prefetches.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool STEAL>
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool STEAL, bool SEG>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
@@ -384,7 +385,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   {
     const uint32_t f = vframe(lane);
     const uint32_t o = f != kNoFrame ? f * 8u : kOOB;
-    uint32_t a = ld_buf<0>(o, off_rsrc), b = ld_buf<8>(o, off_rsrc);
+    uint32_t a = ld_buf<0>(o, off_rsrc);
+    uint32_t b = SEG ? ld_buf<0>(f != kNoFrame ? f * 4u : kOOB, cx.len_rsrc) : ld_buf<8>(o, off_rsrc);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b));
 #pragma unroll
     for (int s = 0; s < S; ++s) fi[s] = f, sb[s] = a, eb[s] = b;
@@ -404,7 +406,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     const uint32_t li = nf + rank - nfv[s];  // < S*NR by construction
     const uint32_t f = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)fi[s]);
     const uint32_t s_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)sb[s]);
-    const uint32_t e_lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)eb[s]);
+    const uint32_t e_raw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(li * 4u), (int)eb[s]);
+    const uint32_t e_lo = SEG ? s_lo + e_raw : e_raw;  // segment mode: eb holds the length
     if (need) {
       if (f != kNoFrame) {
         const uint32_t len = e_lo - s_lo;
@@ -466,7 +469,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     nfv[s] = nf;
     fi[s] = g;
     sb[s] = ld_buf<0>(go, off_rsrc);
-    eb[s] = ld_buf<8>(go, off_rsrc);
+    eb[s] = SEG ? ld_buf<0>(g != kNoFrame ? g * 4u : kOOB, cx.len_rsrc) : ld_buf<8>(go, off_rsrc);
   };
 
   auto compute = [&](auto sc) {
@@ -567,11 +570,12 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // Row width per workgroup from its frames' mean length (RLF = 0), or forced
 // (RLF = 4 / 16, profiling); item size, ring depth and chunk per row width.
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 2, int KS4 = 8, int S4 = 3,
-          int CH16 = 16, int CH4 = 64>
+          int CH16 = 16, int CH4 = 64, bool SEG = false>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
-                  uint64_t* __restrict__ ctrs, uint32_t epoch, uint64_t* __restrict__ timeline) {
+                  uint64_t* __restrict__ ctrs, uint32_t epoch, uint64_t* __restrict__ timeline,
+                  const uint32_t* __restrict__ seg_len) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path
@@ -579,7 +583,13 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   const uint64_t per_block = frames_per_wave * kWavesPerBlock;
   const uint64_t fb0 = (uint64_t)blockIdx.x * per_block < nframes ? (uint64_t)blockIdx.x * per_block : nframes;
   const uint64_t fb1 = fb0 + per_block < nframes ? fb0 + per_block : nframes;
-  const uint64_t ob0 = off[fb0], ob1 = off[fb1];
+  // byte bounds of frames [f0, f1): offsets mode off[f0], off[f1]; segment
+  // mode (frames in address order, not overlapping) start[f0], end of f1 - 1
+  auto lo_of = [&](uint64_t f0, uint64_t f1) -> uint64_t { return SEG ? (f1 > f0 ? off[f0] : 0) : off[f0]; };
+  auto hi_of = [&](uint64_t f0, uint64_t f1) -> uint64_t {
+    return SEG ? (f1 > f0 ? off[f1 - 1] + seg_len[f1 - 1] : 0) : off[f1];
+  };
+  const uint64_t ob0 = lo_of(fb0, fb1), ob1 = hi_of(fb0, fb1);
   bool narrow = RLF == 4;
   if constexpr (RLF == 0) narrow = fb1 > fb0 && ob1 > ob0 && ob1 - ob0 < kShortMean * (fb1 - fb0);
   {
@@ -633,7 +643,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + r.o0 - cx.adj), (short)0,
                                                      (int)((bytes_ + cx.adj + 3) & ~3ull), 0x00020000);
     cx.off_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(off + r.f0), (short)0,
-                                                    (int)((cx.nfb + 1) * 8u), 0x00020000);
+                                                    (int)((cx.nfb + (SEG ? 0u : 1u)) * 8u), 0x00020000);
+    cx.len_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(SEG ? seg_len + r.f0 : seg_len), (short)0,
+                                                    (int)(SEG ? cx.nfb * 4u : 0u), 0x00020000);
     constexpr uint32_t elem = MODE == CrcMode::kCrc ? 4u : 1u;
     cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + r.f0 * elem, (short)0,
                                                     (int)(cx.nfb * elem), 0x00020000);
@@ -650,10 +662,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
-      rows_body<MODE, 4, KS4, S4, CH4, VAR, kSteal>(lds, L, cx);
+      rows_body<MODE, 4, KS4, S4, CH4, VAR, kSteal, SEG>(lds, L, cx);
     } else {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, KS16, S16, CH16, VAR, kSteal>(lds, L, cx);
+      rows_body<MODE, 16, KS16, S16, CH16, VAR, kSteal, SEG>(lds, L, cx);
     }
   };
 
@@ -668,10 +680,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
-      rows_generic<MODE, 4>(lds, L, bytes, off, fw0, fw1, out);
+      rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
     } else {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_generic<MODE, 16>(lds, L, bytes, off, fw0, fw1, out);
+      rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
     }
     if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
     return;
@@ -715,7 +727,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       b = (uint32_t)best;
       const uint64_t f0 = b * per_block < nframes ? b * per_block : nframes;
       const uint64_t f1 = f0 + per_block < nframes ? f0 + per_block : nframes;
-      r = range_of(b, off[f0], off[f1]);
+      r = range_of(b, lo_of(f0, f1), hi_of(f0, f1));
       if (!r.fits) break;  // (marked taken by its owner; cannot happen for a slice with frames left)
     }
   }
@@ -724,7 +736,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
 
 hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                        const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs, uint32_t epoch,
-                       uint64_t* timeline = nullptr) {
+                       uint64_t* timeline = nullptr, const uint32_t* seg_len = nullptr) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
   uint64_t grid = (n + per_block - 1) / per_block;
@@ -735,8 +747,10 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, ctrs, \
-                     epoch, timeline)
-  if (verify) {
+                     epoch, timeline, seg_len)
+  if (seg_len) {  // segment mode (lnx_crc32_segments; the TX FCS append)
+    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 8, 3, 16, 64, true);
+  } else if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
     switch (var) {
@@ -770,6 +784,10 @@ hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* o
                                 const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs,
                                 uint32_t epoch, uint64_t* timeline) {
   return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, ctrs, epoch, timeline);
+}
+hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                                 void* out, const void* images, int num_cus, hipStream_t stream) {
+  return launch_rows(0, false, bytes, start, n, out, images, num_cus, stream, nullptr, 0, nullptr, len);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

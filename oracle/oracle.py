@@ -275,6 +275,22 @@ def ingress_verdict(frame: bytes, flags: int = 0) -> int:
     return 0
 
 
+# ------------------------------------------------------------ TX FCS append
+ERR_SHORT_BUFFER = 6
+
+
+def fcs_append(frame: bytes, capacity: int) -> tuple[bytes, int]:
+    """Tail of StackEthernet.Encapsulate with the CRC32Update hook set
+    (internet/stack-ethernet.go:200-214): zero-pad to 60 bytes, append
+    LE32(crc32.Update(0, IEEETable, frame)).  A frame that would outgrow
+    `capacity` is returned unchanged with ErrShortBuffer (the per-frame form of
+    the destination-size check at internet/stack-ethernet.go:170-179)."""
+    padded = frame + bytes(max(0, 60 - len(frame)))
+    if len(padded) + 4 > capacity:
+        return frame, ERR_SHORT_BUFFER
+    return padded + struct.pack("<I", crc32_update(0, padded)), 0
+
+
 # ----------------------------------------------------------------- C oracle
 _lib = None
 

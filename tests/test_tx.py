@@ -1,0 +1,66 @@
+"""TX FCS append (internet/stack-ethernet.go:200-214) and the
+segment form of the batch CRC, on frames in fixed-size ring slots."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+CAP = 1536
+
+
+def test_oracle_append_matches_reference_shape():
+    f, st = O.fcs_append(b"\x01" * 10, CAP)
+    assert st == 0 and len(f) == 64 and f[10:60] == bytes(50)
+    assert O.crc32_search(f, 0) == 60                 # crc_test.go: the FCS is found right after the data
+    assert O.crc32(f) == 0x2144DF1C                    # residue of a frame with its FCS
+    f, st = O.fcs_append(b"\x02" * 1500, CAP)
+    assert st == 0 and len(f) == 1504 and O.crc32_search(f, 0) == 1500
+    f, st = O.fcs_append(b"\x03" * (CAP - 3), CAP)
+    assert st == O.ERR_SHORT_BUFFER and len(f) == CAP - 3
+
+
+def _slots(rng, n):
+    lens = rng.integers(0, CAP + 1, size=n).astype(np.int64)
+    lens[::7] = rng.integers(0, 61, size=len(lens[::7]))       # runts: padding path
+    lens[::11] = CAP - rng.integers(0, 8, size=len(lens[::11]))  # near capacity: short-buffer path
+    data = rng.integers(0, 256, size=n * CAP, dtype=np.uint8)
+    return data, lens
+
+
+@pytest.mark.gpu
+def test_gpu_fcs_append(cuda):
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(31)
+    n = 5000
+    data, lens = _slots(rng, n)
+    starts = np.arange(n, dtype=np.int64) * CAP
+    d = torch.from_numpy(data.copy()).to(cuda)
+    ds = torch.from_numpy(starts).to(cuda)
+    dl = torch.from_numpy(lens.astype(np.int32)).to(cuda)
+    status = L.fcs_append_batch(d, ds, dl, CAP).cpu().numpy()
+    got, got_len = d.cpu().numpy(), dl.cpu().numpy()
+    for i in range(n):
+        frame = data[i * CAP: i * CAP + int(lens[i])].tobytes()
+        want, st = O.fcs_append(frame, CAP)
+        assert int(status[i]) == st, i
+        assert int(got_len[i]) == len(want), i
+        assert got[i * CAP: i * CAP + len(want)].tobytes() == want, i
+        # bytes past the new frame end are untouched
+        assert np.array_equal(got[i * CAP + len(want): (i + 1) * CAP], data[i * CAP + len(want): (i + 1) * CAP]), i
+
+
+@pytest.mark.gpu
+def test_gpu_crc32_segments(cuda):
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(32)
+    n = 20000
+    stride = rng.integers(1, 3000, size=n)
+    lens = np.minimum(stride, rng.integers(0, 3000, size=n))
+    starts = np.concatenate([[3], 3 + np.cumsum(stride)[:-1]]).astype(np.int64)
+    data = rng.integers(0, 256, size=int(starts[-1] + stride[-1] + 8), dtype=np.uint8)
+    got = L.crc32_segments(torch.from_numpy(data).to(cuda), torch.from_numpy(starts).to(cuda),
+                           torch.from_numpy(lens.astype(np.int32)).to(cuda)).cpu().numpy().view(np.uint32)
+    want = [O.crc32(data[s:s + l].tobytes()) for s, l in zip(starts, lens)]
+    assert got.tolist() == want
