@@ -94,6 +94,16 @@ inline int VerifyFCSBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64
                           void* stream = nullptr) {
   return lnx_fcs_verify_batch(d_frames, d_off, n, d_ok, stream);
 }
+// Frames in ring slots: CRC32 of bytes[start[i] : start[i] + len[i]].
+inline int CRC32Segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
+                         uint32_t* d_crc, void* stream = nullptr) {
+  return lnx_crc32_segments(d_bytes, d_start, d_len, n, d_crc, stream);
+}
+// CRC32Search over every capture bytes[off[i] : off[i+1]] (ethernet/crc.go:28-47).
+inline int CRC32SearchBatch(const uint8_t* d_bytes, const uint64_t* d_off, const int64_t* d_minOffCRC, uint64_t n,
+                            int64_t* d_found, void* stream = nullptr) {
+  return lnx_crc32_search_batch(d_bytes, d_off, d_minOffCRC, n, d_found, stream);
+}
 
 }  // namespace ethernet
 
@@ -161,5 +171,19 @@ inline size_t AppendFCS(uint8_t* frame, size_t n, const StackEthernetConfig& c) 
     n += 4;
   }
   return n;
+}
+
+// Batch form of AppendFCS with CRC32Update set, in place on frames in ring
+// slots of `capacity` bytes (status 6 = lneto.ErrShortBuffer).
+inline int AppendFCSBatch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n,
+                          uint32_t capacity, uint8_t* d_status, void* stream = nullptr) {
+  return lnx_fcs_append_batch(d_bytes, d_start, d_len, n, capacity, d_status, stream);
+}
+
+// Receive-path checksum verdicts of every Ethernet frame (0 or the lneto
+// errGeneric code), StackEthernet.Demux -> demux4 / demux6.
+inline int VerifyIngressBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_verdict,
+                              bool evilBit = false, void* stream = nullptr) {
+  return lnx_ingress_verify_batch(d_frames, d_off, n, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, d_verdict, stream);
 }
 }  // namespace internet
