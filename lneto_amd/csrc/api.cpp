@@ -1,6 +1,7 @@
 // api.cpp — C-ABI of the batched HIP path: per-device context (the LDS table
 // image), argument checks, host-memory and multi-GPU conveniences.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -13,11 +14,9 @@
 
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                               bool verify, const void* image, int num_cus, hipStream_t stream, uint64_t* ctrs,
-                               uint32_t epoch);
+                               bool verify, const void* image, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* image, int num_cus, hipStream_t stream, uint64_t* ctrs,
-                                uint32_t epoch, uint64_t* timeline);
+                                const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream);
@@ -76,53 +75,32 @@ int hip_fail(hipError_t e, const char* what) {
   return LNX_EHIP;
 }
 
-// Chunk counters of the CRC kernel's stealing mode (crc32_kernel.hip): one
-// set of per-workgroup 64-bit counters per stream, tagged with a per-set epoch
-// that grows by one per launch.  Launches on one stream run in order, so a set
-// is never used by two launches at once; a stream beyond kCtrSets runs in
-// workgroup mode (no stealing) instead.
-constexpr int kCtrSets = 64;
-constexpr int kCtrPerSet = 1024;  // >= workgroups of a launch (one per CU)
-
 struct DeviceCtx {
   std::once_flag once;
   int status = LNX_OK;
   void* d_image = nullptr;
   int num_cus = 0;
-  uint64_t* d_ctrs = nullptr;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
-  std::mutex mu;
-  void* set_stream[kCtrSets] = {};
-  uint32_t set_epoch[kCtrSets] = {};
-  int sets_used = 0;
 };
-
-// Counter set and epoch for a launch on `stream` (nullptr / 0: workgroup mode).
-void ctr_set_for(DeviceCtx* c, void* stream, uint64_t** ctrs, uint32_t* epoch) {
-  *ctrs = nullptr;
-  *epoch = 0;
-  if (!c->d_ctrs) return;
-  std::lock_guard<std::mutex> lk(c->mu);
-  int k = 0;
-  while (k < c->sets_used && c->set_stream[k] != stream) ++k;
-  if (k == c->sets_used) {
-    if (k == kCtrSets) return;
-    c->set_stream[k] = stream;
-    ++c->sets_used;
-  }
-  if (c->set_epoch[k] == 0xFFFFFFFFu) return;  // epoch space used up on this stream
-  *epoch = ++c->set_epoch[k];
-  *ctrs = c->d_ctrs + (size_t)k * kCtrPerSet;
-}
 
 constexpr int kMaxDevices = 64;
 DeviceCtx g_ctx[kMaxDevices];
 
-// Both images back to back: [RL = 16][RL = 4] (lds_layout.hpp image_index).
+// Compact form of an image (lds_layout.hpp kCompactDwords): the U values once,
+// then the F/T tail verbatim.
+std::vector<uint32_t> compact_image(const std::vector<uint32_t>& full) {
+  std::vector<uint32_t> c(kCompactDwords);
+  for (uint32_t m = 0; m < 4; ++m)
+    for (uint32_t e = 0; e < 256; ++e) c[256 * m + e] = full[u_addr(m, e, 0) / 4];
+  std::copy(full.begin() + kFBase / 4, full.end(), c.begin() + kCompactUDwords);
+  return c;
+}
+
+// Both compact images back to back: [RL = 16][RL = 4] (lds_layout.hpp image_index).
 const std::vector<uint32_t>& host_image() {
   static const std::vector<uint32_t> img = [] {
-    std::vector<uint32_t> all = build_lds_image(16);
-    const std::vector<uint32_t> i4 = build_lds_image(4);
+    std::vector<uint32_t> all = compact_image(build_lds_image(16));
+    const std::vector<uint32_t> i4 = compact_image(build_lds_image(4));
     all.insert(all.end(), i4.begin(), i4.end());
     return all;
   }();
@@ -144,11 +122,6 @@ int get_ctx(DeviceCtx** out) {
     if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(image)"); return; }
     err = hipMemcpy(c.d_image, img.data(), img.size() * 4, hipMemcpyHostToDevice);
     if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(image)"); return; }
-    const size_t ctr_bytes = sizeof(uint64_t) * kCtrSets * kCtrPerSet;
-    err = hipMalloc(reinterpret_cast<void**>(&c.d_ctrs), ctr_bytes);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(counters)"); return; }
-    err = hipMemset(c.d_ctrs, 0, ctr_bytes);  // epoch 0: stale for every launch
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemset(counters)"); return; }
     const std::vector<uint32_t> st = build_search_tables();
     err = hipMalloc(reinterpret_cast<void**>(&c.d_search), st.size() * 4);
     if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(search tables)"); return; }
@@ -167,13 +140,8 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  // Workgroup mode: in stealing mode the in-order vmcnt makes every slot wait
-  // behind the chunk claim's device-scope atomic, which cost 12 % at 1500 B
-  // (DESIGN.md §3.1); the stealing path stays reachable as variants 200+.
-  uint64_t* ctrs = nullptr;
-  uint32_t epoch = 0;
   hipError_t e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
-                                     static_cast<hipStream_t>(stream), ctrs, epoch);
+                                     static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "crc32_frames_kernel launch");
   return LNX_OK;
 }
@@ -332,11 +300,8 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  uint64_t* ctrs = nullptr;
-  uint32_t epoch = 0;
-  if (var >= 200 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);  // 200+: stealing mode
-  hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream), ctrs, epoch, nullptr);
+  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
   return LNX_OK;
 }
@@ -351,11 +316,8 @@ int64_t lnx__crc32_timeline(int var, const uint8_t* d_bytes, const uint64_t* d_o
   if (st != LNX_OK) return st;
   if (!d_timeline) return (int64_t)crc32_launch_waves(n, c->num_cus);
   if (n == 0 || !d_bytes || !d_off || !d_crc) return LNX_EINVAL;
-  uint64_t* ctrs = nullptr;
-  uint32_t epoch = 0;
-  if (var >= 200 && c->num_cus <= kCtrPerSet) ctr_set_for(c, stream, &ctrs, &epoch);
-  hipError_t e = launch_crc32_variant(var % 100, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream), ctrs, epoch, d_timeline);
+  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                      static_cast<hipStream_t>(stream), d_timeline);
   if (e != hipSuccess) return hip_fail(e, "crc32 timeline launch");
   return LNX_OK;
 }

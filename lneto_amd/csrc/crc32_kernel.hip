@@ -279,27 +279,10 @@ __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* byt
 // rel(x) = x - off[fb0] + adj, frame indices relative to fb0.
 struct WaveCtx {
   uint32_t nfb, o0_lo, adj;  // frames of the range, low dword of its first offset, alignment
-  uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase), workgroup mode
-  uint64_t* gctr;            // global chunk counter of the range (epoch << 32 | claimed), stealing mode
-  uint32_t gctr_off, epoch;  // byte offset of gctr in ctr_rsrc; this launch's epoch
-  __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc, ctr_rsrc;
+  uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase)
+  __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc;
   __amdgpu_buffer_rsrc_t len_rsrc;  // segment mode: the length array
 };
-
-// One returning 64-bit atomic add of v on the counter at byte voff, or (no
-// claim) a 64-bit load from an out-of-range offset: either way exactly one
-// vmcnt event, so the ring's count stays static.
-__device__ __forceinline__ void claim_or_nop(bool claim, bool leader, uint64_t& r, uint32_t voff, uint64_t v,
-                                             __amdgpu_buffer_rsrc_t rsrc) {
-  if (claim) {
-    if (leader) {  // one lane: a wave instruction with one active lane is still one vmcnt event
-      r = v;
-      asm volatile("s_nop 4\n\tbuffer_atomic_add_x2 %0, %1, %2, 0 offen sc0" : "+v"(r) : "v"(voff), "s"(rsrc));
-    }
-  } else {
-    asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen" : "=v"(r) : "v"(kOOB), "s"(rsrc));
-  }
-}
 
 // RL: lanes per row, KS: window steps per item, S: ring slots, CH: frames per
 // chunk, VAR: profiling knob (0 = product, 1 = loads +
@@ -313,46 +296,45 @@ __device__ __forceinline__ void claim_or_nop(bool claim, bool leader, uint64_t& 
 // sees its chunks as one virtual frame sequence v = 0, 1, ...: it holds the
 // bases of the chunk v is in (bc) and of the next one (bn), which covers the
 // S*NR-frame bounds window every slot prefetches.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool STEAL, bool SEG>
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
   constexpr uint32_t kSbLog = RL == 16 ? 6 : 4;
   static_assert(RL == 4 || RL == 16, "row width");
-  static_assert(S >= 2 && S * NR <= (uint32_t)CH && CH <= 64, "bounds window within two chunks");
+  static_assert(S >= 1 && NR <= (uint32_t)CH && CH <= 64 && S * NR <= 64, "chunk and bounds window shape");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
-  // a claim issued at one chunk boundary has landed (S slots later) before the next
-  static_assert(!STEAL || (uint32_t)CH >= (S + 1) * NR, "claim latency");
-  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3 + (STEAL ? 1 : 0);  // steps, junk, start + end, claim
+  constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3;  // steps, junk, start + end
+  // bounds window: only lanes < S*NR are ever read back (ds_bpermute index
+  // li < S*NR); the other lanes' offset loads are out of range (VAR 3: all 64
+  // lanes load, the earlier behaviour, for A/B timing)
+  constexpr uint32_t kWin = VAR == 3 ? 64u : S * NR;
   constexpr int kPending = (S - 1) * kLoads;       // loads issued after a slot's own
   const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bf = L.bf, bt = L.bt;
   const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
   const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
 
-  // ---- chunks (uniform)
-  // a claimed count of another epoch (cannot happen after the range's epoch
-  // init) is treated as exhausted
-  auto count_of = [&](uint64_t old) -> uint32_t {
-    return (uint32_t)(old >> 32) == cx.epoch ? (uint32_t)old : nfb;
-  };
-  auto claim = [&]() -> uint32_t {  // synchronous: outside the ring only, or in workgroup mode
+  // ---- chunks (uniform): one ds_add_rtn on the workgroup's LDS counter
+  auto claim = [&]() -> uint32_t {
     uint32_t b = 0;
-    if constexpr (STEAL) {
-      if (lane == 0) b = count_of(__hip_atomic_fetch_add(cx.gctr, (uint64_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    } else {
-      if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, (uint32_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, (uint32_t)CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
-  uint32_t cc = 0;          // virtual chunk index of bc
-  uint32_t bc = claim();    // first frame of chunk cc
-  uint32_t bn = claim();    // first frame of chunk cc + 1
-  uint32_t bnn = STEAL ? claim() : 0u;  // stealing mode: chunk cc + 2, claimed ahead asynchronously
-  int pend = -1;            // slot whose claim is in flight (stealing mode)
-  uint64_t cl[S];           // per-slot claim result registers
+  // The bounds window [nf, nf + S*NR) starts inside chunk cc, so it touches
+  // chunks cc .. cc + NB - 1; their first frames are held in cb[].
+  constexpr uint32_t NB = 1 + (CH + S * NR - 2) / CH;
+  static_assert((CH & (CH - 1)) == 0, "power-of-two chunks");
+  constexpr uint32_t kChLog = __builtin_ctz(CH);
+  uint32_t cc = 0;          // virtual chunk index of cb[0]
+  uint32_t cb[NB];          // first frame of chunk cc + k
+#pragma unroll
+  for (uint32_t k = 0; k < NB; ++k) cb[k] = claim();
   auto vframe = [&](uint32_t v) -> uint32_t {  // frame of virtual index v, kNoFrame past the work
-    const uint32_t c0 = cc * CH;
-    const uint32_t f = v < c0 + CH ? bc + (v - c0) : (v < c0 + 2 * CH ? bn + (v - c0 - CH) : kNoFrame);
+    const uint32_t r = v - cc * CH;  // v >= cc * CH
+    const uint32_t k = r >> kChLog;
+    uint32_t f = kNoFrame;
+#pragma unroll
+    for (uint32_t i = 0; i < NB; ++i) f = k == i ? cb[i] + (r & (CH - 1)) : f;
     return f < nfb ? f : kNoFrame;
   };
 
@@ -375,7 +357,6 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 #pragma unroll
     for (int k = 0; k < KS; ++k) w[s][k] = 0;
     jk[s] = 0;
-    cl[s] = 0;
     it_f[s] = kNoFrame;
     it_n[s] = it_t[s] = it_j0[s] = it_ns[s] = 0;
     hw[s] = false;
@@ -383,7 +364,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   }
   // first bounds window for every slot (drained before the loop)
   {
-    const uint32_t f = vframe(lane);
+    const uint32_t f = lane < kWin ? vframe(lane) : kNoFrame;
     const uint32_t o = f != kNoFrame ? f * 8u : kOOB;
     uint32_t a = ld_buf<0>(o, off_rsrc);
     uint32_t b = SEG ? ld_buf<0>(f != kNoFrame ? f * 4u : kOOB, cx.len_rsrc) : ld_buf<8>(o, off_rsrc);
@@ -449,22 +430,13 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }
     jk[s] = ld_buf<0>(jv, data_rsrc);
     // 4. bounds of the next S*NR frames, for this slot's next issue
-    bool claim_now = false;
     if (nf >= (cc + 1) * CH) {  // at most one chunk boundary per issue (cnt <= NR <= CH)
       ++cc;
-      bc = bn;
-      if constexpr (STEAL) {
-        bn = bnn;  // landed: claimed at the previous boundary, >= S slots ago
-        claim_now = true;
-      } else {
-        bn = claim();
-      }
+#pragma unroll
+      for (uint32_t k = 0; k + 1 < NB; ++k) cb[k] = cb[k + 1];
+      cb[NB - 1] = claim();
     }
-    if constexpr (STEAL) {
-      claim_or_nop(claim_now, lane == 0, cl[s], cx.gctr_off, (uint64_t)CH, cx.ctr_rsrc);
-      if (claim_now) pend = s;
-    }
-    const uint32_t g = vframe(nf + lane);
+    const uint32_t g = lane < kWin ? vframe(nf + lane) : kNoFrame;
     const uint32_t go = g != kNoFrame ? g * 8u : kOOB;
     nfv[s] = nf;
     fi[s] = g;
@@ -475,13 +447,6 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   auto compute = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     slot_wait<kPending, KS>(w[s], jk[s], sb[s], eb[s]);
-    if constexpr (STEAL) {
-      asm volatile("" : "+v"(cl[s]));
-      if (pend == s) {
-        bnn = (uint32_t)__builtin_amdgcn_readfirstlane((int)count_of(cl[s]));
-        pend = -1;
-      }
-    }
     const uint32_t n = it_n[s], t = it_t[s], ns = it_ns[s], j0 = it_j0[s];
     const uint32_t J = n ? (n + t + SB - 1) >> kSbLog : 0u;
     const bool alive = it_f[s] != kNoFrame;
@@ -569,12 +534,12 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // ------------------------------------------------------------------ kernel
 // Row width per workgroup from its frames' mean length (RLF = 0), or forced
 // (RLF = 4 / 16, profiling); item size, ring depth and chunk per row width.
-template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 2, int KS4 = 8, int S4 = 3,
-          int CH16 = 16, int CH4 = 64, bool SEG = false>
+template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 1, int KS4 = 16, int S4 = 1,
+          int CH16 = 4, int CH4 = 16, bool SEG = false>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
-                  uint64_t* __restrict__ ctrs, uint32_t epoch, uint64_t* __restrict__ timeline,
+                  uint64_t* __restrict__ timeline,
                   const uint32_t* __restrict__ seg_len) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
@@ -593,12 +558,28 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   bool narrow = RLF == 4;
   if constexpr (RLF == 0) narrow = fb1 > fb0 && ob1 > ob0 && ob1 - ob0 < kShortMean * (fb1 - fb0);
   {
-    // the image is zero at kCtrBase, which starts the chunk counter at 0
-    const uint4* img = images + (narrow ? image_index(4) : image_index(16)) * (kLdsBytes / 16);
-    uint4* l4 = reinterpret_cast<uint4*>(lds_words);
+    // compact image (lds_layout.hpp): thread t expands U value t into its 32
+    // bank replicas (128 contiguous bytes, eight 16-byte writes started at a
+    // lane-rotated position so the wave's writes spread over the banks), then
+    // the F/T tail is copied verbatim; it is zero at kCtrBase, which starts
+    // the chunk counter at 0
+    static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
+    const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
+                          (narrow ? image_index(4) : image_index(16)) * kCompactDwords;
+    const uint32_t t = threadIdx.x;
+    const uint32_t uv = img[t];
+    const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
+    constexpr int kTail = (int)((kLdsBytes - kFBase) / 16 / kBlockThreads);
+    uint4 tv[kTail];
 #pragma unroll
-    for (int i = 0; i < (int)(kLdsBytes / 16 / kBlockThreads); ++i)
-      l4[threadIdx.x + i * kBlockThreads] = img[threadIdx.x + i * kBlockThreads];
+    for (int i = 0; i < kTail; ++i) tv[i] = tail[t + i * kBlockThreads];
+    uint4* urow = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_words) + u_addr(t >> 8, t & 255u, 0));
+    const uint4 u4 = {uv, uv, uv, uv};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) urow[(i + t) & 7u] = u4;
+    uint4* l4 = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_words) + kFBase);
+#pragma unroll
+    for (int i = 0; i < kTail; ++i) l4[t + i * kBlockThreads] = tv[i];
   }
 
   const uint32_t lane = threadIdx.x & 63u;
@@ -649,33 +630,13 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     constexpr uint32_t elem = MODE == CrcMode::kCrc ? 4u : 1u;
     cx.out_rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(out) + r.f0 * elem, (short)0,
                                                     (int)(cx.nfb * elem), 0x00020000);
-    cx.ctr_rsrc = __builtin_amdgcn_make_buffer_rsrc(ctrs, (short)0, (int)(gridDim.x * 8u), 0x00020000);
     cx.o0_lo = (uint32_t)r.o0;
     cx.ctr = lds_words + kCtrBase / 4;
-    cx.gctr = nullptr;
-    cx.gctr_off = 0;
-    cx.epoch = epoch;
     return cx;
   };
-  auto run = [&](const WaveCtx& cx, auto steal) {
-    constexpr bool kSteal = decltype(steal)::value;
-    asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
-    if (narrow) {
-      L.p = lane & 3u, L.row = lane >> 2;
-      rows_body<MODE, 4, KS4, S4, CH4, VAR, kSteal, SEG>(lds, L, cx);
-    } else {
-      L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, KS16, S16, CH16, VAR, kSteal, SEG>(lds, L, cx);
-    }
-  };
-
   const Range own = range_of(blockIdx.x, ob0, ob1);
   if (!own.fits) {
-    // gigabyte frames: static per-wave ranges on the unpipelined path; thieves
-    // are told this slice is taken
-    if (ctrs && lane == 0)
-      __hip_atomic_fetch_max(ctrs + blockIdx.x, ((uint64_t)epoch << 32) | 0xFFFFFFFFull, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    // gigabyte frames: static per-wave ranges on the unpipelined path
     const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow) {
@@ -685,58 +646,24 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       L.p = lane & 15u, L.row = lane >> 4;
       rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
     }
-    if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
-    return;
-  }
-  if (!ctrs) {
-    // workgroup mode: chunks of the own slice from the LDS counter
-    run(ctx_of(own), std::false_type{});
   } else {
-    // stealing mode: chunks of the own slice from its global counter, then of
-    // the slice with the most frames left, until none has 2 chunks left
-    constexpr uint32_t kMinSteal = 2 * (uint32_t)(CH16 > CH4 ? CH16 : CH4);
-    uint64_t b = blockIdx.x;
-    Range r = own;
-    for (;;) {
-      WaveCtx cx = ctx_of(r);
-      cx.gctr = ctrs + b;
-      cx.gctr_off = (uint32_t)b * 8u;
-      uint64_t seen = 0;  // epoch init: a stale count (older epoch) becomes (epoch, 0)
-      if (lane == 0) seen = __hip_atomic_fetch_max(cx.gctr, (uint64_t)epoch << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("" ::"v"(seen));
-      run(cx, std::true_type{});
-      // the slice with the most frames left (lane-parallel scan of the counters)
-      uint64_t best = 0;
-      for (uint32_t w = lane; w < gridDim.x; w += 64) {
-        const uint64_t f0 = (uint64_t)w * per_block < nframes ? (uint64_t)w * per_block : nframes;
-        const uint64_t f1 = f0 + per_block < nframes ? f0 + per_block : nframes;
-        const uint64_t c = __hip_atomic_load(ctrs + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t claimed = (uint32_t)(c >> 32) == epoch ? (uint32_t)c : 0u;
-        const uint64_t left = claimed < f1 - f0 ? f1 - f0 - claimed : 0u;
-        const uint64_t key = (left << 32) | w;
-        best = key > best ? key : best;
-      }
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) {
-        const uint64_t o = (uint64_t)__shfl_xor((unsigned long long)best, m, 64);
-        best = o > best ? o : best;
-      }
-      best = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(best >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)best);
-      if ((best >> 32) < kMinSteal) break;
-      b = (uint32_t)best;
-      const uint64_t f0 = b * per_block < nframes ? b * per_block : nframes;
-      const uint64_t f1 = f0 + per_block < nframes ? f0 + per_block : nframes;
-      r = range_of(b, lo_of(f0, f1), hi_of(f0, f1));
-      if (!r.fits) break;  // (marked taken by its owner; cannot happen for a slice with frames left)
+    // chunks of the own slice from the LDS counter
+    const WaveCtx cx = ctx_of(own);
+    asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
+    if (narrow) {
+      L.p = lane & 3u, L.row = lane >> 2;
+      rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
+    } else {
+      L.p = lane & 15u, L.row = lane >> 4;
+      rows_body<MODE, 16, KS16, S16, CH16, VAR, SEG>(lds, L, cx);
     }
   }
   if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                       const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs, uint32_t epoch,
-                       uint64_t* timeline = nullptr, const uint32_t* seg_len = nullptr) {
+                       const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr,
+                       const uint32_t* seg_len = nullptr) {
   if (n == 0) return hipSuccess;
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
   uint64_t grid = (n + per_block - 1) / per_block;
@@ -746,27 +673,35 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const uint4* img = static_cast<const uint4*>(images);
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
-  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, ctrs, \
-                     epoch, timeline, seg_len)
+  hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
+                     timeline, seg_len)
   if (seg_len) {  // segment mode (lnx_crc32_segments; the TX FCS append)
-    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 8, 3, 16, 64, true);
+    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 4, 16, true);
   } else if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
+    // profiling variants (tools/prof/variants.py).  Arguments:
+    // VAR, forced row width (0 = per workgroup), KS16, S16, KS4, S4, CH16, CH4
     switch (var) {
-      // profiling variants (tools/prof/variants.py)
-      case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;              // loads + bookkeeping only
-      case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;              // lookups + bookkeeping only
-      case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2); break;  // forced 16-lane rows
-      case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3); break;
-      case 28: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 12); break;  // 12-frame chunks
-      case 29: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 8, 3, 32); break;  // 32-frame chunks
-      case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 8, 3); break;  // forced 4-lane rows
-      case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 16, 3); break;
-      case 24: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 12, 2); break;
-      case 25: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 2, 6, 3); break;
-      case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4, 24, 2, 8, 3); break;  // 4-lane rows, loads only
-      case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4, 24, 2, 8, 3); break;  // 4-lane rows, math only
+      case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
+      case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
+      case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
+      case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16); break;  // forced 16-lane rows
+      case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
+      case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;  // forced 4-lane rows
+      case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 8, 3, 4, 64); break;
+      case 24: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 32); break;
+      case 25: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 6, 3, 4, 64); break;
+      case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
+      case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
+      case 29: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 16, 1, 32, 16); break;  // 32-frame chunks
+      case 30: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 8, 3, 16, 64); break;  // round-1 product: two-slot rings
+      case 31: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 8, 16); break;  // two-slot ring, 8-frame chunks
+      case 33: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 4, 16); break;  // two-slot ring, 4-frame chunks
+      case 39: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 12, 2, 16, 1, 4, 16); break;  // 12-step items
+      case 43: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 1, 4, 16); break;  // 12-step short items
+      case 45: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16); break;
+      case 47: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 8, 32); break;
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
     }
   }
@@ -776,18 +711,16 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
 
 // Host-side launch helpers (called from api.cpp).
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                               const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs,
-                               uint32_t epoch) {
-  return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream, ctrs, epoch);
+                               const void* images, int num_cus, hipStream_t stream) {
+  return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream);
 }
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                                const void* images, int num_cus, hipStream_t stream, uint64_t* ctrs,
-                                uint32_t epoch, uint64_t* timeline) {
-  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, ctrs, epoch, timeline);
+                                const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
+  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, timeline);
 }
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, false, bytes, start, n, out, images, num_cus, stream, nullptr, 0, nullptr, len);
+  return launch_rows(0, false, bytes, start, n, out, images, num_cus, stream, nullptr, len);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

@@ -60,4 +60,12 @@ constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // 
 static_assert(t_addr(31, 1, 3, 15) < kCtrBase, "T region overlaps the counter");
 constexpr int image_index(int rl) { return rl == 16 ? 0 : 1; }
 
+// Compact image in HBM (what a workgroup reads at start): the 1024 distinct U
+// values U_m[e] at dword 256m + e, then the [kFBase, kLdsBytes) tail of the
+// LDS image verbatim (F, T, the zero counter).  The kernel writes each U value
+// into its 32 bank replicas itself, so a workgroup reads 36 KiB instead of
+// 160 KiB before its first frame load.
+constexpr uint32_t kCompactUDwords = 1024;
+constexpr uint32_t kCompactDwords = kCompactUDwords + (kLdsBytes - kFBase) / 4;
+
 }  // namespace lnx

@@ -17,10 +17,10 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# 20/21: 16-lane rows (KS, S) = (24, 2), (12, 3); 28/29: (24, 2) with 12 / 32-frame chunks;
-# 200 + id: the same in stealing mode (global chunk counters, idle workgroups steal)
-# 22..25: 4-lane rows (8,3), (16,3), (12,2), (6,3)
-FORCED = [20, 21, 22, 23, 24, 25, 28, 29, 200, 220, 222]
+# 20/21: forced 16-lane rows, (KS, S) = (24, 1), (12, 3); 29: (24, 2) with 32-frame chunks;
+# 22..25: forced 4-lane rows (16, 1), (8, 3), (12, 2), (6, 3);
+# 30/31/33/39/43/45/47: per-workgroup row width with other item / ring / chunk shapes
+FORCED = [20, 21, 22, 23, 24, 25, 29, 30, 31, 33, 39, 43, 45, 47]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

@@ -1,8 +1,15 @@
-"""Time the CRC kernel's profiling variants on the 1M x 1500 B batch.
-0 = product kernel, 1 = loads + bookkeeping only, 2 = lookups + bookkeeping only."""
+"""Time the CRC kernel's profiling variants on one workload.
+0 = product kernel, 1 = loads + bookkeeping only, 2 = lookups + bookkeeping only
+(other numbers: crc32_kernel.hip launch_rows).  The GPU is warmed for ~0.5 s
+first (the first few hundred microseconds of launches run at lower clocks),
+then the variants are timed round-robin REPS times and the median is printed,
+so box drift hits every variant alike.
+
+usage: variants.py WORKLOAD V1,V2,... [REPS]"""
 import ctypes
 import sys
 import os
+import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch
@@ -20,22 +27,40 @@ d = synth.bytes_torch(int(off[-1]), dev)
 o = torch.from_numpy(off.astype(np.int64)).to(dev)
 out = torch.empty(n, dtype=torch.int32, device=dev)
 s = torch.cuda.current_stream()
-vars_ = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2, 0]
-NOT_CRC = {1, 2, 26, 27}  # timing-only variants (loads only / math only)
+vars_ = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2]
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+NOT_CRC = {1, 2, 26, 27, 32, 34, 38}  # timing-only variants (loads only / math only)
 ref = torch.empty_like(out)
 L.crc32_batch(d, o, out=ref)
 torch.cuda.synchronize()
 print(f"lib {L.LIB_PATH}")
-for var in vars_:
-    for _ in range(3):
-        L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream)
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record(s)
+
+
+def launch(var):
+    assert L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream) == 0
+
+
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < 0.5:
     for _ in range(20):
-        L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream)
-    ev[1].record(s)
+        launch(0)
     torch.cuda.synchronize()
-    ms = ev[0].elapsed_time(ev[1]) / 20
-    ok = "" if var in NOT_CRC else ("  crc ok" if torch.equal(out, ref) else "  CRC MISMATCH")
-    print(f"{wl} variant {var}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s{ok}")
+res = {v: [] for v in vars_}
+ok = {}
+for r in range(reps):
+    for var in vars_:
+        launch(var)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(s)
+        for _ in range(20):
+            launch(var)
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        res[var].append(ev[0].elapsed_time(ev[1]) / 20)
+        if var not in NOT_CRC:
+            ok[var] = ok.get(var, True) and torch.equal(out, ref)
+for var in vars_:
+    ms = float(np.median(res[var]))
+    tag = "" if var in NOT_CRC else ("  crc ok" if ok[var] else "  CRC MISMATCH")
+    spread = " ".join(f"{x:.4f}" for x in res[var])
+    print(f"{wl} variant {var}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s{tag}   [{spread}]", flush=True)
