@@ -218,14 +218,17 @@ __device__ __forceinline__ void slot_wait(uint32_t (&w)[KS], uint32_t& junk, uin
 
 enum class CrcMode : int { kCrc = 0, kVerify = 1 };
 
+// The result of frame f: its CRC, or (verify mode) 1 if the residue matches.
 template <CrcMode MODE>
-__device__ __forceinline__ void store_result(__amdgpu_buffer_rsrc_t out_rsrc, bool st, uint32_t f, uint32_t n,
-                                             uint32_t crc) {
+__device__ __forceinline__ uint32_t result_of(uint32_t n, uint32_t crc) {
+  return MODE == CrcMode::kCrc ? crc : ((n >= 4 && crc == 0x2144DF1Cu) ? 1u : 0u);
+}
+template <CrcMode MODE>
+__device__ __forceinline__ void store_result(__amdgpu_buffer_rsrc_t out_rsrc, bool st, uint32_t f, uint32_t v) {
   if (MODE == CrcMode::kCrc)
-    __builtin_amdgcn_raw_buffer_store_b32(crc, out_rsrc, st ? f * 4u : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, out_rsrc, st ? f * 4u : kOOB, 0, 0);
   else
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((n >= 4 && crc == 0x2144DF1Cu) ? 1 : 0), out_rsrc,
-                                         st ? f : kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, st ? f : kOOB, 0, 0);
 }
 
 // Per-lane constants.
@@ -375,6 +378,19 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 
   uint32_t reg = 0;  // this lane's CRC register for its row's frame in progress
   int live = 0;      // slots holding work
+  // 4-lane rows hold their results in registers and write them RL at a time:
+  // lane p of a row holds the row's p-th finished frame (hf) and its result
+  // (hv); pc counts them.  That saves stores where a wave finishes up to 16
+  // frames per slot (short frames, VALU-bound: 3 % on the Zipf mix).  16-lane
+  // rows store every slot instead: their held flushes write 16-byte pieces of
+  // output lines at uncorrelated times, and the partial-line writebacks cost
+  // 3 % at 1500 B, more than the per-slot stores (variant 4 vs 0).
+  constexpr bool kHold = RL == 4 && VAR != 4;
+  uint32_t hf = 0, hv = 0, pc = 0;
+  auto flush = [&]() {
+    store_result<MODE>(out_rsrc, p < pc, hf, hv);
+    pc = 0;
+  };
 
   auto issue = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
@@ -444,7 +460,14 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     eb[s] = SEG ? ld_buf<0>(g != kNoFrame ? g * 4u : kOOB, cx.len_rsrc) : ld_buf<8>(go, off_rsrc);
   };
 
-  auto compute = [&](auto sc) {
+  // A slot's frames after its fold, carried over the next issue: the finish
+  // (F_p, row XOR, Z_{-t}, store) runs after the slot's next loads are out,
+  // so its LDS round trips overlap them instead of idling the wave.
+  struct Fin {
+    uint32_t reg, junk, f, n, t;
+    bool last, any;
+  };
+  auto compute = [&](auto sc) -> Fin {
     constexpr int s = decltype(sc)::value;
     slot_wait<kPending, KS>(w[s], jk[s], sb[s], eb[s]);
     const uint32_t n = it_n[s], t = it_t[s], ns = it_ns[s], j0 = it_j0[s];
@@ -489,19 +512,37 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         }
       }
     }
+    Fin fin;
+    fin.reg = reg;
+    fin.junk = jk[s] & ~(uint32_t)(0xFFFFFFFFull >> (8 * t));
+    fin.f = it_f[s];
+    fin.n = n;
+    fin.t = t;
+    fin.last = last;
+    fin.any = wave_any(last);
+    return fin;
+  };
+  auto finish = [&](const Fin& fin) {
     uint32_t crc = 0;
-    if (wave_any(last)) {
+    const uint32_t n = fin.n, t = fin.t;
+    if (fin.any) {
       // the last lane absorbed t junk bytes past the frame end: take their
-      // U-image out (jk is 0 on every other lane, and U(0) = 0)
-      const uint32_t junk = jk[s] & ~(uint32_t)(0xFFFFFFFFull >> (8 * t));
-      const uint32_t r = reg ^ u_step(lds, junk, bu0, bu1);
+      // U-image out (junk is 0 on every other lane, and U(0) = 0)
+      const uint32_t r = fin.reg ^ u_step(lds, fin.junk, bu0, bu1);
       uint32_t R = t_fix<RL>(lds, row_xor<RL>(f_step(lds, r, bf)), t, p, bt);
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
       crc = ~R;
     }
-    // one store per slot, outside any branch: static vmcnt count
-    store_result<MODE>(out_rsrc, last && p == 0, it_f[s], n, crc);
+    // hold the result; a flush adds a vmcnt event after the slot's loads,
+    // which only makes the waits of rows_body stricter
+    if constexpr (!kHold) {
+      store_result<MODE>(out_rsrc, fin.last && p == 0, fin.f, result_of<MODE>(n, crc));
+    } else {
+      if (fin.last && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
+      pc += fin.last ? 1u : 0u;
+      if (wave_any(pc == (uint32_t)RL)) flush();
+    }
   };
 
 #define LNX_FENCE __builtin_amdgcn_sched_barrier(0)
@@ -509,16 +550,18 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   auto slot = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (done) return;
-    compute(sc);
+    const Fin fin = compute(sc);
     live -= hw[s] ? 1 : 0;
     const bool more = vframe(nf) != kNoFrame || wave_any(rj < rJ);
     if (live == 0 && !more) {
       done = true;
+      finish(fin);
       return;
     }
     LNX_FENCE;
     issue(sc);
     LNX_FENCE;
+    finish(fin);
     live += hw[s] ? 1 : 0;
   };
   while (!done) {
@@ -527,6 +570,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }(std::make_integer_sequence<int, S>{});
   }
 #undef LNX_FENCE
+  if (kHold && wave_any(pc != 0)) flush();
   // drain: no asm load may still be writing registers when the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -534,7 +578,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // ------------------------------------------------------------------ kernel
 // Row width per workgroup from its frames' mean length (RLF = 0), or forced
 // (RLF = 4 / 16, profiling); item size, ring depth and chunk per row width.
-template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 1, int KS4 = 16, int S4 = 1,
+template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 1, int KS4 = 12, int S4 = 2,
           int CH16 = 4, int CH4 = 16, bool SEG = false>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
@@ -676,7 +720,7 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
                      timeline, seg_len)
   if (seg_len) {  // segment mode (lnx_crc32_segments; the TX FCS append)
-    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 4, 16, true);
+    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true);
   } else if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
@@ -686,6 +730,7 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
       case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
+      case 4: LNX_LAUNCH(CrcMode::kCrc, 4); break;  // one result store per slot for 4-lane rows too
       case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;  // forced 4-lane rows
@@ -700,8 +745,12 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 33: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 4, 16); break;  // two-slot ring, 4-frame chunks
       case 39: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 12, 2, 16, 1, 4, 16); break;  // 12-step items
       case 43: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 1, 4, 16); break;  // 12-step short items
-      case 45: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16); break;
+      case 45: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 4, 16); break;  // one-slot 16-step short items
       case 47: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 8, 32); break;
+      case 48: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 16, 16); break;
+      case 49: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 32, 16); break;
+      case 50: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 16, 16); break;
+      case 51: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 32, 16); break;
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
     }
   }

@@ -17,7 +17,7 @@
 // bytes, as crc32_rows_kernel reads); LD 2: LD 1 through inline-asm raw buffer
 // loads from one voffset + immediates (the kernel's instruction form).
 #define L6(k) "buffer_load_dword %" #k ", %24, %25, 0 offen offset:" #k "*64\n\t"
-template <int MODE, int CH, int LD = 0>
+template <int MODE, int CH, int LD = 0, int EX = 0>
 __global__ void __launch_bounds__(1024) walk(const uint8_t* __restrict__ base, uint64_t nframes, uint32_t fb,
                                              uint32_t* out) {
   __shared__ uint32_t pad[40950];
@@ -28,9 +28,22 @@ __global__ void __launch_bounds__(1024) walk(const uint8_t* __restrict__ base, u
   const uint32_t w = threadIdx.x >> 6;
   const uint64_t per_block = (nframes + gridDim.x - 1) / gridDim.x;
   const uint64_t b0 = blockIdx.x * per_block, b1 = std::min<uint64_t>(b0 + per_block, nframes);
-  uint32_t acc = 0;
+  uint32_t acc = 0, held = 0, nheld = 0;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)(nframes * fb), 0x00020000);
+  // EX bits (LD 2 only): 1 = two offset loads per batch (lanes 0..7, 8-byte
+  // stride, like the kernel's bounds window), 2 = one 4-byte store per row per
+  // batch, 4 = a 160 KiB LDS fill from global memory at start
+  if (EX & 4) {
+    const uint4* src = reinterpret_cast<const uint4*>(base);
+    uint4* l4 = reinterpret_cast<uint4*>(pad);
+    for (int i = threadIdx.x; i < 40950 / 4; i += 1024) l4[i] = src[i];
+    __syncthreads();
+  }
+  const __amdgpu_buffer_rsrc_t osr =
+      __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(nframes * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), (short)0, (int)(nframes * 8 + 8), 0x00020000);
   auto frame4 = [&](uint64_t f) {
     uint32_t v[24];
     if (LD == 0) {
@@ -59,9 +72,34 @@ __global__ void __launch_bounds__(1024) walk(const uint8_t* __restrict__ base, u
                      "=v"(v[15]), "=v"(v[16]), "=v"(v[17]), "=v"(v[18]), "=v"(v[19]), "=v"(v[20]), "=v"(v[21]),
                      "=v"(v[22]), "=v"(v[23])
                    : "v"(vo), "s"(rsrc));
+      if (EX & 1) {
+        uint32_t a, b;
+        const uint32_t oo = lane < 8 ? (uint32_t)(f * 8 + lane * 8) : 0x80000000u;
+        asm volatile("s_nop 4\n\tbuffer_load_dword %0, %2, %3, 0 offen\n\tbuffer_load_dword %1, %2, %3, 0 offen offset:8\n\ts_waitcnt vmcnt(0)"
+                     : "=v"(a), "=v"(b) : "v"(oo), "s"(orsrc));
+        v[0] ^= a ^ b;
+      }
     }
 #pragma unroll
     for (int u = 0; u < 24; ++u) acc ^= v[u];
+    if (EX & 2) {
+      const uint32_t so = (p == 0 && f < b1) ? (uint32_t)(f * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(acc, osr, so, 0, 0);
+    }
+    if (EX & 8) {  // one 64-lane dword store (256 B contiguous) every 64 frames
+      if (((f - row) & 63) == 0) {
+        const uint32_t so = f + 64 <= b1 ? (uint32_t)(f * 4 + lane * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(acc, osr, so, 0, 0);
+      }
+    }
+    if (EX & 32) {  // keep the result; written once at the end (below)
+      held = held * 31u + acc;
+      ++nheld;
+    }
+    if (EX & 16) {  // per-batch store, non-temporal
+      const uint32_t so = (p == 0 && f < b1) ? (uint32_t)(f * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(acc, osr, so, 0, 2);
+    }
   };
   if (MODE == 0) {
     const uint64_t pw = (b1 - b0 + 15) / 16;
@@ -77,6 +115,14 @@ __global__ void __launch_bounds__(1024) walk(const uint8_t* __restrict__ base, u
       c = __builtin_amdgcn_readfirstlane(c);
       if (b0 + c >= b1) break;
       for (uint32_t k = 0; k < CH; k += 4) frame4(b0 + c + k + row);
+    }
+  }
+  if (EX & 32) {  // the same byte count as per-batch stores, in one burst at the end
+    const uint64_t gw = (uint64_t)blockIdx.x * 16 + w;
+    const uint64_t per_wave = nframes / (gridDim.x * 16);
+    for (uint32_t k = 0; k < per_wave; k += 64) {
+      const uint32_t so = (gw * per_wave + k + lane) < nframes ? (uint32_t)((gw * per_wave + k + lane) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(held + k, osr, so, 0, 0);
     }
   }
   pad[threadIdx.x] = acc;
@@ -99,12 +145,12 @@ int main(int argc, char** argv) {
   const uint32_t fb = argc > 1 ? (uint32_t)atoi(argv[1]) : 1536;
   const uint64_t nframes = 1 << 20;
   uint8_t* buf; uint32_t* out;
-  (void)hipMalloc(&buf, nframes * fb + 4096); (void)hipMalloc(&out, 64);
+  (void)hipMalloc(&buf, nframes * fb + 4096); (void)hipMalloc(&out, nframes * 4 + 64);
   (void)hipMemset(buf, 3, nframes * fb);
-#define RUN(M, C, LD) { float ms = tm([&] { walk<M, C, LD><<<256, 1024>>>(buf, nframes, fb, out); }); \
-  printf("fb=%u mode=%d CH=%3d LD=%d : %.4f ms %.1f GB/s\n", fb, M, C, LD, ms, nframes * fb / ms / 1e6); }
+#define RUN(M, C, LD, EX) { float ms = tm([&] { walk<M, C, LD, EX><<<256, 1024>>>(buf, nframes, fb, out); }); \
+  printf("fb=%u mode=%d CH=%3d LD=%d EX=%d : %.4f ms %.1f GB/s\n", fb, M, C, LD, EX, ms, nframes * fb / ms / 1e6); }
   for (int rep = 0; rep < 2; ++rep) {
-    RUN(0, 4, 0); RUN(2, 4, 0); RUN(2, 16, 0); RUN(2, 4, 1); RUN(2, 16, 1); RUN(2, 4, 2); RUN(2, 16, 2);
+    RUN(2, 4, 2, 0); RUN(2, 4, 2, 2); RUN(2, 4, 2, 32); RUN(2, 4, 2, 0); RUN(2, 4, 2, 2); RUN(2, 4, 2, 32);
   }
   return 0;
 }
