@@ -165,6 +165,45 @@ int lnx_crc32_batch_multi(int ngpu, const int* devices, const uint8_t* const* d_
                           const uint64_t* const* d_off_per_gpu, const uint64_t* n_per_gpu,
                           uint32_t* const* d_crc_per_gpu);
 
+/* ======================================================================== *
+ * 3. Receive ring: pinned slots + batched FCS verify / ingress verdicts
+ *    
+ * ======================================================================== */
+
+/* A pool of `nslots` receive slots of `slot_cap` bytes in pinned host memory,
+ * modelled on netdev's bufferSelect (x/netdev/buffer.go:25-37: fixed slots, a
+ * length per slot), with `depth` device pipeline stages of `batch_slots`
+ * slots each (batch_slots * slot_cap < 2 GiB; 0 = nslots).  A producer writes
+ * frames straight into the slots (lnx_rx_ring_slots) and their buffer lengths
+ * into lnx_rx_ring_lengths.  slot_cap must be a multiple of 4. */
+typedef struct lnx_rx_ring lnx_rx_ring;
+int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t batch_slots, uint32_t depth,
+                       lnx_rx_ring** out);
+void lnx_rx_ring_destroy(lnx_rx_ring* ring);
+/* Pinned slot memory: slot i is bytes [i*slot_cap, (i+1)*slot_cap). */
+uint8_t* lnx_rx_ring_slots(lnx_rx_ring* ring);
+/* Pinned buffer length per slot (bytes of slot i in use, <= slot_cap). */
+uint32_t* lnx_rx_ring_lengths(lnx_rx_ring* ring);
+
+/* netdev.Stack.IngressPackets (x/netdev/interface.go:82-89;
+ * xnet.Netstack.IngressPackets, x/xnet/netstack.go:103-111) for slots
+ * [first, first + count): the frame of slot i is slot[offset : len_i] and
+ * carries its 4-byte LE FCS.  fcs_ok[k] = 1 iff that FCS is right (the check
+ * lneto leaves to the PHY, x/netdev/interface.go:34-40); verdict[k] = the
+ * receive path's checksum-stage verdict of the frame with the FCS stripped,
+ * as lnx_ingress_verify_batch.  Host output arrays of `count` entries (either
+ * may be NULL).  Synchronous; internally the slot range is pipelined over the
+ * ring's stages (H2D, kernels, D2H on one HIP stream per stage). */
+int lnx_rx_ring_ingress(lnx_rx_ring* ring, uint32_t first, uint32_t count, uint32_t offset, uint32_t flags,
+                        uint8_t* fcs_ok, uint8_t* verdict);
+
+/* The same for caller-owned buffers, exactly IngressPackets(bufs, offset):
+ * frame k = bufs[k][offset : lens[k]] (lens[k] <= slot_cap).  The buffers are
+ * gathered into the ring's slots (parallel host copies, overlapped with the
+ * device work of the previous batch); nothing is retained after the call. */
+int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
+                        uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict);
+
 /* Number of visible HIP devices (0 when none). */
 int lnx_device_count(void);
 

@@ -21,7 +21,7 @@ import os
 __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
-    "crc32_batch_host", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE",
+    "crc32_batch_host", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE", "RxRing",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -73,6 +73,15 @@ _sig = {
     "lnx_fcs_append_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
     "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "lnx_rx_ring_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    "lnx_rx_ring_destroy": (None, [_vp]),
+    "lnx_rx_ring_slots": (_vp, [_vp]),
+    "lnx_rx_ring_lengths": (_vp, [_vp]),
+    "lnx_rx_ring_ingress": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           _vp, _vp]),
+    "lnx_ingress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           _vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
     "lnx_last_error": (ctypes.c_char_p, []),
     "lnx_version": (ctypes.c_char_p, []),
@@ -293,6 +302,64 @@ def crc32_batch_host(h_bytes, h_off, device: int = 0):
         _check(lib.lnx_crc32_batch_host(h_bytes.ctypes.data, h_bytes.nbytes, h_off.ctypes.data, n,
                                         out.ctypes.data, device), "lnx_crc32_batch_host")
     return out[:max(n, 0)]
+
+
+class RxRing:
+    """Pinned receive ring + batched FCS verify / ingress verdicts (lnx_rx_ring_*,
+    SURVEY.md §8(f).1), the batch form of netdev.Stack.IngressPackets
+    (x/netdev/interface.go:82-89) over bufferSelect-style slots (x/netdev/buffer.go).
+
+    ``slots`` is a (nslots, slot_cap) uint8 numpy view of the pinned slot memory
+    and ``lengths`` a uint32 view of the per-slot buffer lengths: a producer
+    writes frames (with their FCS) there, then ``ingress(first, count, offset)``
+    returns (fcs_ok, verdict) uint8 arrays.  ``ingress_packets(bufs, offset)``
+    takes caller-owned buffers instead (IngressPackets(bufs, offset) exactly).
+    """
+
+    def __init__(self, nslots: int, slot_cap: int = 2048, batch_slots: int = 0, depth: int = 3, device: int = 0):
+        import numpy as np
+        h = _vp()
+        _check(lib.lnx_rx_ring_create(device, nslots, slot_cap, batch_slots, depth, ctypes.byref(h)),
+               "lnx_rx_ring_create")
+        self._h = h
+        self.nslots, self.slot_cap = nslots, slot_cap
+        sp = lib.lnx_rx_ring_slots(h)
+        lp = lib.lnx_rx_ring_lengths(h)
+        self.slots = np.ctypeslib.as_array((ctypes.c_uint8 * (nslots * slot_cap)).from_address(sp)).reshape(
+            nslots, slot_cap)
+        self.lengths = np.ctypeslib.as_array((ctypes.c_uint32 * nslots).from_address(lp))
+
+    def ingress(self, first: int = 0, count: int | None = None, offset: int = 0, flags: int = 0):
+        import numpy as np
+        if count is None:
+            count = self.nslots - first
+        ok = np.zeros(max(count, 1), dtype=np.uint8)
+        verdict = np.zeros(max(count, 1), dtype=np.uint8)
+        _check(lib.lnx_rx_ring_ingress(self._h, first, count, offset, flags, ok.ctypes.data, verdict.ctypes.data),
+               "lnx_rx_ring_ingress")
+        return ok[:count], verdict[:count]
+
+    def ingress_packets(self, bufs, offset: int = 0, flags: int = 0):
+        import numpy as np
+        arrs = [np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray)
+                else np.ascontiguousarray(b, dtype=np.uint8) for b in bufs]
+        n = len(arrs)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data if a.size else None for a in arrs])
+        lens = np.array([a.size for a in arrs] or [0], dtype=np.uint32)
+        ok = np.zeros(max(n, 1), dtype=np.uint8)
+        verdict = np.zeros(max(n, 1), dtype=np.uint8)
+        _check(lib.lnx_ingress_packets(self._h, ptrs, lens.ctypes.data, n, offset, flags, ok.ctypes.data,
+                                       verdict.ctypes.data), "lnx_ingress_packets")
+        return ok[:n], verdict[:n]
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self.slots = self.lengths = None
+            lib.lnx_rx_ring_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 def device_count() -> int:

@@ -19,7 +19,8 @@ hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* o
                                 const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
-                                 uint8_t* verdict, int num_cus, hipStream_t stream);
+                                 uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
+                                 uint32_t trim);
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
@@ -147,6 +148,19 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
 }
 
 }  // namespace
+
+// For the other translation units (rx_ring.hip): the current device's LDS
+// image and CU count, and the thread's lnx_last_error.
+int device_resources(const void** image, int* num_cus) {
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  *image = c->d_image;
+  *num_cus = c->num_cus;
+  return LNX_OK;
+}
+int hip_error(hipError_t e, const char* what) { return hip_fail(e, what); }
+
 }  // namespace lnx
 
 using namespace lnx;
@@ -228,7 +242,7 @@ int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags, d_verdict, c->num_cus,
-                                       static_cast<hipStream_t>(stream));
+                                       static_cast<hipStream_t>(stream), nullptr, 0);
   if (e != hipSuccess) return hip_fail(e, "ingress_verify_kernel launch");
   return LNX_OK;
 }

@@ -719,8 +719,11 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
 #define LNX_LAUNCH(M, ...) \
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
                      timeline, seg_len)
-  if (seg_len) {  // segment mode (lnx_crc32_segments; the TX FCS append)
-    LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true);
+  if (seg_len) {  // segment mode (lnx_crc32_segments, the TX FCS append, the receive ring)
+    if (verify)
+      LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
+    else
+      LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true);
   } else if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
@@ -770,6 +773,10 @@ hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* o
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream) {
   return launch_rows(0, false, bytes, start, n, out, images, num_cus, stream, nullptr, len);
+}
+hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                                      uint8_t* ok, const void* images, int num_cus, hipStream_t stream) {
+  return launch_rows(0, true, bytes, start, n, ok, images, num_cus, stream, nullptr, len);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

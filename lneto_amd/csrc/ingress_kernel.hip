@@ -62,13 +62,19 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
 
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
-                      uint32_t flags, uint8_t* __restrict__ verdict) {
+                      uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
+                      uint32_t trim) {
+  // offsets mode (seg_len null): frame f = bytes[off[f] : off[f+1]]; segment
+  // mode (the receive ring): frame f = bytes[off[f] : off[f] + seg_len[f] - trim],
+  // i.e. the FCS (trim = 4) is stripped, empty if seg_len[f] < trim
   const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kIngBlock / 64);
   for (uint64_t q = (uint64_t)blockIdx.x * (kIngBlock / 64) + (threadIdx.x >> 6); q * 4 < n; q += nwaves) {
     const uint64_t f = q * 4 + row;
     const bool live = f < n;
-    const uint64_t s = live ? off[f] : 0, e = live ? off[f + 1] : 0;
+    const uint64_t s = live ? off[f] : 0;
+    const uint32_t sl = live && seg_len ? seg_len[f] : 0u;
+    const uint64_t e = !live ? 0 : (seg_len ? s + (sl > trim ? sl - trim : 0u) : off[f + 1]);
     const uint64_t len64 = e > s ? e - s : 0;
     const uint32_t L = len64 < 0x7FFFFFFFull ? (uint32_t)len64 : 0x7FFFFFFFu;
     const uint8_t* fr = bytes + s;
@@ -109,6 +115,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
 
     // ---- header parse: row-uniform; v = verdict so far, sums requested below
     uint32_t v = 0;
+    uint32_t v_udp4 = 0;  // IPv4 UDP size verdict: demux4 reports it only after the header sum passed
     bool hdr_sum = false, l4_sum = false;
     int32_t pa = 0, pb = 0, la = 0, lb = 0;  // pseudo-address bytes [pa, pb), transport [la, lb)
     uint32_t lseed = 0;                       // length + protocol words of the pseudo-header
@@ -140,11 +147,11 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               lseed = ((tl - hl) & 0xFFFFu) + 6u;
             } else if (proto == 17) {
               if (P < 8) {
-                v = kErrTruncatedFrame;
+                v_udp4 = kErrTruncatedFrame;
               } else {
                 const uint32_t ul = field16(14 + hl + 4);
-                if (ul < 8) v = kErrInvalidLengthField;
-                else if (ul > P) v = kErrTruncatedFrame;
+                if (ul < 8) v_udp4 = kErrInvalidLengthField;
+                else if (ul > P) v_udp4 = kErrTruncatedFrame;
                 else {
                   l4_sum = true;
                   pa = 26, pb = 34, la = 14 + hl, lb = 14 + hl + ul;
@@ -210,20 +217,22 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     }
     hE = row_add(hE), hO = row_add(hO), tE = row_add(tE), tO = row_add(tO);
     if (v == 0 && hdr_sum && ing_sum16(256u * hE + hO) != 0) v = kErrBadCRC;
+    if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
     if (v == 0 && l4_sum && ing_sum16(256u * tE + tO + lseed) != 0) v = kErrBadCRC;
     if (live && p == 0) verdict[f] = (uint8_t)v;
   }
 }
 
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
-                                 uint8_t* verdict, int num_cus, hipStream_t stream) {
+                                 uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
+                                 uint32_t trim) {
   if (n == 0) return hipSuccess;
   const uint64_t frames_per_block = (kIngBlock / 64) * 4;
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL(ingress_verify_kernel, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n, flags,
-                     verdict);
+                     verdict, seg_len, trim);
   return hipGetLastError();
 }
 

@@ -1,0 +1,272 @@
+// rx_ring.hip — pinned receive ring and the batched ingress pipeline.
+//
+// Reference: netdev.Stack.IngressPackets(bufs [][]byte, offset int) error
+// (x/netdev/interface.go:82-89), implemented by xnet.Netstack
+// (x/xnet/netstack.go:103-111) as one StackEthernet.Demux per buffer
+// (internet/stack-ethernet.go:139-165) with buf[offset:] as the frame.  The
+// buffers come from netdev's bufferSelect slot pool (x/netdev/buffer.go:25-37:
+// fixed slots of a fixed capacity, a length per slot).  lneto never checks the
+// FCS (the PHY is trusted, x/netdev/interface.go:34-40); here the ring checks
+// it before the stack sees the frame, and computes the receive path's
+// checksum-stage verdict of the stripped frame in the same pass.
+//
+// The ring owns `nslots` slots of `slot_cap` bytes in pinned host memory
+// (hipHostMalloc) plus a pinned length per slot, so a producer (tap / NIC
+// queue) writes frames where the GPU can DMA them.  lnx_rx_ring_ingress runs a
+// slot range through `depth` stages, each on its own HIP stream with its own
+// device buffers; batch k uses stage k % depth:
+//     H2D  slots [b0, b0 + nb) (one contiguous copy) and their lengths
+//     ring_segments_kernel   start = i*cap + offset, len = min(len, cap) - offset
+//     crc32_rows_kernel      segment mode, FCS residue verify  -> ok[i]
+//     ingress_verify_kernel  segment mode, FCS stripped       -> verdict[i]
+//     D2H  ok / verdict into pinned result arrays
+// so the copy of batch k+1 overlaps the kernels of batch k: the pipeline runs
+// at the PCIe rate, the kernels are ~100x faster than the link.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include "../../include/lneto_amd.h"
+
+namespace lnx {
+
+int device_resources(const void** image, int* num_cus);
+int hip_error(hipError_t e, const char* what);
+hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                                      uint8_t* ok, const void* images, int num_cus, hipStream_t stream);
+hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
+                                 uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
+                                 uint32_t trim);
+
+// Slot i of the batch: frame = slot[offset : min(len, cap)].
+__global__ void __launch_bounds__(256)
+ring_segments_kernel(uint64_t* __restrict__ start, uint32_t* __restrict__ len, uint32_t n, uint32_t cap,
+                     uint32_t offset) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t l = len[i] < cap ? len[i] : cap;
+    start[i] = (uint64_t)i * cap + offset;
+    len[i] = l > offset ? l - offset : 0u;
+  }
+}
+
+}  // namespace lnx
+
+using namespace lnx;
+
+struct lnx_rx_ring {
+  int device = 0;
+  uint32_t nslots = 0, cap = 0, batch = 0, depth = 0;
+  uint8_t* h_slots = nullptr;
+  uint32_t* h_len = nullptr;
+  uint8_t* h_ok = nullptr;
+  uint8_t* h_verdict = nullptr;
+  struct Stage {
+    hipStream_t s = nullptr;
+    uint8_t* d_bytes = nullptr;
+    uint64_t* d_start = nullptr;
+    uint32_t* d_len = nullptr;
+    uint8_t* d_ok = nullptr;
+    uint8_t* d_verdict = nullptr;
+  };
+  std::vector<Stage> st;
+  const void* image = nullptr;
+  int num_cus = 0;
+  std::mutex mu;  // one ingress call at a time (the stages are shared)
+};
+
+namespace {
+
+void ring_free(lnx_rx_ring* r) {
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  for (auto& s : r->st) {
+    if (s.s) (void)hipStreamSynchronize(s.s);
+    (void)hipFree(s.d_bytes);
+    (void)hipFree(s.d_start);
+    (void)hipFree(s.d_len);
+    (void)hipFree(s.d_ok);
+    (void)hipFree(s.d_verdict);
+    if (s.s) (void)hipStreamDestroy(s.s);
+  }
+  (void)hipHostFree(r->h_slots);
+  (void)hipHostFree(r->h_len);
+  (void)hipHostFree(r->h_ok);
+  (void)hipHostFree(r->h_verdict);
+  delete r;
+}
+
+// Enqueue slots [b0, b0 + nb) on stage `s` (asynchronous).
+int enqueue(lnx_rx_ring* r, lnx_rx_ring::Stage& s, uint32_t b0, uint32_t nb, uint32_t offset, uint32_t flags) {
+  hipError_t e;
+  const size_t cap = r->cap;
+  if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
+                          s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+    return hip_error(e, "rx ring H2D");
+  const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
+  hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
+  if ((e = launch_fcs_verify_segments(s.d_bytes, s.d_start, s.d_len, nb, s.d_ok, r->image, r->num_cus, s.s)) !=
+      hipSuccess)
+    return hip_error(e, "rx ring FCS verify launch");
+  if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, flags, s.d_verdict, r->num_cus, s.s, s.d_len, 4)) !=
+      hipSuccess)
+    return hip_error(e, "rx ring ingress verify launch");
+  if ((e = hipMemcpyAsync(r->h_ok + b0, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->h_verdict + b0, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
+    return hip_error(e, "rx ring D2H");
+  return LNX_OK;
+}
+
+int sync_all(lnx_rx_ring* r) {
+  int rc = LNX_OK;
+  for (auto& s : r->st) {
+    const hipError_t e = hipStreamSynchronize(s.s);
+    if (e != hipSuccess && rc == LNX_OK) rc = hip_error(e, "rx ring hipStreamSynchronize");
+  }
+  return rc;
+}
+
+void copy_out(const lnx_rx_ring* r, uint32_t first, uint32_t count, uint8_t* fcs_ok, uint8_t* verdict) {
+  if (fcs_ok) std::memcpy(fcs_ok, r->h_ok + first, count);
+  if (verdict) std::memcpy(verdict, r->h_verdict + first, count);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t batch_slots, uint32_t depth,
+                       lnx_rx_ring** out) {
+  if (!out) return LNX_EINVAL;
+  *out = nullptr;
+  if (nslots == 0 || slot_cap == 0 || slot_cap % 4 != 0 || depth == 0 || depth > 8) return LNX_EINVAL;
+  if (batch_slots == 0 || batch_slots > nslots) batch_slots = nslots;
+  if ((uint64_t)batch_slots * slot_cap >= (1ull << 31)) return LNX_EINVAL;  // one segment-mode slice per batch
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return LNX_ENODEV;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+  auto* r = new lnx_rx_ring;
+  r->device = device, r->nslots = nslots, r->cap = slot_cap, r->batch = batch_slots, r->depth = depth;
+  int rc = device_resources(&r->image, &r->num_cus);
+  if (rc != LNX_OK) { ring_free(r); return rc; }
+  const size_t slots_bytes = (size_t)nslots * slot_cap;
+  if ((e = hipHostMalloc(reinterpret_cast<void**>(&r->h_slots), slots_bytes, hipHostMallocDefault)) != hipSuccess ||
+      (e = hipHostMalloc(reinterpret_cast<void**>(&r->h_len), (size_t)nslots * 4, hipHostMallocDefault)) !=
+          hipSuccess ||
+      (e = hipHostMalloc(reinterpret_cast<void**>(&r->h_ok), nslots, hipHostMallocDefault)) != hipSuccess ||
+      (e = hipHostMalloc(reinterpret_cast<void**>(&r->h_verdict), nslots, hipHostMallocDefault)) != hipSuccess) {
+    rc = hip_error(e, "hipHostMalloc(rx ring)");
+    ring_free(r);
+    return rc;
+  }
+  std::memset(r->h_len, 0, (size_t)nslots * 4);
+  r->st.resize(depth);
+  for (auto& s : r->st) {
+    if ((e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_bytes), (size_t)batch_slots * slot_cap)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_start), (size_t)batch_slots * 8)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_len), (size_t)batch_slots * 4)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_ok), batch_slots)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_verdict), batch_slots)) != hipSuccess) {
+      rc = hip_error(e, "rx ring stage allocation");
+      ring_free(r);
+      return rc;
+    }
+  }
+  *out = r;
+  return LNX_OK;
+}
+
+void lnx_rx_ring_destroy(lnx_rx_ring* ring) { ring_free(ring); }
+
+uint8_t* lnx_rx_ring_slots(lnx_rx_ring* ring) { return ring ? ring->h_slots : nullptr; }
+uint32_t* lnx_rx_ring_lengths(lnx_rx_ring* ring) { return ring ? ring->h_len : nullptr; }
+
+int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t offset, uint32_t flags,
+                        uint8_t* fcs_ok, uint8_t* verdict) {
+  if (!r) return LNX_EINVAL;
+  if ((uint64_t)first + count > r->nslots || offset >= r->cap) return LNX_EINVAL;
+  if (count == 0) return LNX_OK;
+  std::lock_guard<std::mutex> lk(r->mu);
+  hipError_t e = hipSetDevice(r->device);
+  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+  int rc = LNX_OK;
+  uint32_t k = 0;
+  for (uint32_t b0 = first; b0 < first + count && rc == LNX_OK; b0 += r->batch, ++k) {
+    const uint32_t nb = std::min(r->batch, first + count - b0);
+    rc = enqueue(r, r->st[k % r->depth], b0, nb, offset, flags);
+  }
+  const int rs = sync_all(r);
+  if (rc == LNX_OK) rc = rs;
+  if (rc == LNX_OK) copy_out(r, first, count, fcs_ok, verdict);
+  return rc;
+}
+
+int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
+                        uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict) {
+  if (!r || (n > 0 && (!bufs || !lens))) return LNX_EINVAL;
+  if (offset >= r->cap) return LNX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (lens[i] > r->cap || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
+  if (n == 0) return LNX_OK;
+  std::lock_guard<std::mutex> lk(r->mu);
+  hipError_t e = hipSetDevice(r->device);
+  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+  // Batches go round-robin over the stages; batch k gathers into the slot
+  // block of stage k % depth, after that stage's previous batch has drained.
+  // The gather (host memcpy, parallel) of batch k+1 overlaps the copies and
+  // kernels of batch k.
+  const uint32_t per = std::max<uint32_t>(1, std::min(r->batch, r->nslots / r->depth));
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  int rc = LNX_OK;
+  std::vector<std::pair<uint64_t, uint32_t>> pending(r->depth, {0, 0});  // (first frame, count) per stage
+  auto drain = [&](uint32_t k) {
+    const hipError_t se = hipStreamSynchronize(r->st[k].s);
+    if (se != hipSuccess) return hip_error(se, "rx ring hipStreamSynchronize");
+    const uint64_t f0 = pending[k].first;
+    const uint32_t cnt = pending[k].second;
+    if (fcs_ok) std::memcpy(fcs_ok + f0, r->h_ok + (size_t)k * per, cnt);
+    if (verdict) std::memcpy(verdict + f0, r->h_verdict + (size_t)k * per, cnt);
+    pending[k].second = 0;
+    return LNX_OK;
+  };
+  uint64_t i0 = 0;
+  for (uint32_t k = 0; i0 < n && rc == LNX_OK; ++k, i0 += per) {
+    const uint32_t sk = k % r->depth;
+    if (pending[sk].second) rc = drain(sk);
+    if (rc != LNX_OK) break;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
+    const uint32_t s0 = sk * per;
+    auto gather = [&](uint32_t a, uint32_t b) {
+      for (uint32_t j = a; j < b; ++j) {
+        const uint32_t l = lens[i0 + j];
+        if (l) std::memcpy(r->h_slots + (size_t)(s0 + j) * r->cap, bufs[i0 + j], l);
+        r->h_len[s0 + j] = l;
+      }
+    };
+    const uint32_t nth = nb >= 4096 ? hw : 1;
+    if (nth == 1) {
+      gather(0, nb);
+    } else {
+      std::vector<std::thread> th;
+      for (uint32_t t = 0; t < nth; ++t)
+        th.emplace_back(gather, (uint32_t)((uint64_t)nb * t / nth), (uint32_t)((uint64_t)nb * (t + 1) / nth));
+      for (auto& t : th) t.join();
+    }
+    rc = enqueue(r, r->st[sk], s0, nb, offset, flags);
+    pending[sk] = {i0, nb};
+  }
+  for (uint32_t k = 0; k < r->depth; ++k) {
+    if (!pending[k].second) continue;
+    const int d = drain(k);
+    if (rc == LNX_OK) rc = d;
+  }
+  return rc;
+}
+
+}  // extern "C"

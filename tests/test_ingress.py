@@ -123,3 +123,43 @@ def test_gpu_ingress_reference_frames(cuda):
     got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda),
                                  torch.from_numpy(off.astype(np.int64)).to(cuda)).cpu().numpy()
     assert got.tolist() == [0, 0, 0, O.ERR_BAD_CRC]
+
+
+def _header_then_udp_frames():
+    """Corrupted IPv4 header AND a broken UDP size: demux4 checks the header sum
+    (internet/stack-ip4.go:128-131) before udp.NewFrame / ValidateSize (:150-158),
+    so the verdict is ErrBadCRC, not the UDP size error."""
+    out = []
+    for pay, ulen in [(b"", 7), (b"ab", 11), (b"abcdef", 40), (b"", None)]:
+        for cut in (0, 4):
+            good = G.ether(0x0800, G.ipv4(17, G.udp(pay, length=ulen)))
+            if cut:  # transport shorter than a UDP header: tl shrunk with the frame
+                b = bytearray(good[:14 + 20 + 4])
+                b[16:18] = (24).to_bytes(2, "big")
+                b[24:26] = b"\0\0"
+                b[24:26] = O.ipv4_header_sum16(bytes(b[14:34])).to_bytes(2, "big")
+                good = bytes(b)
+            out.append(good)
+            bad = bytearray(good)
+            bad[22] ^= 0x01  # TTL: header sum breaks, lengths stay
+            out.append(bytes(bad))
+    return out
+
+
+def test_header_sum_precedes_udp_size_checks():
+    codes = [O.ingress_verdict(f) for f in _header_then_udp_frames()]
+    assert codes[1::2] == [O.ERR_BAD_CRC] * (len(codes) // 2)
+    assert set(codes[0::2]) >= {O.ERR_INVALID_LENGTH_FIELD, O.ERR_TRUNCATED_FRAME}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base_pad", [0, 3])
+def test_gpu_header_sum_precedes_udp_size_checks(cuda, base_pad):
+    import torch
+    import lneto_amd as L
+    frames = _header_then_udp_frames()
+    data, off = _pack(frames, base_pad)
+    got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda),
+                                 torch.from_numpy(off.astype(np.int64)).to(cuda)).cpu().numpy()
+    want = [O.ingress_verdict(f) for f in frames]
+    assert got.tolist() == want

@@ -1,0 +1,150 @@
+"""Receive ring: pinned slots -> H2D -> FCS verify + receive-path
+verdicts -> D2H, the batch form of netdev.Stack.IngressPackets(bufs, offset)
+(x/netdev/interface.go:82-89, x/xnet/netstack.go:103-111).
+
+Every frame carries its LE FCS (internet/stack-ethernet.go:211-214).  Expected
+values come from the oracle: fcs_ok = CRC32(frame) == residue (len >= 4), verdict
+= oracle.ingress_verdict(frame without its FCS)."""
+import struct
+
+import numpy as np
+import pytest
+
+import lneto_amd as L
+from oracle import oracle as O
+from tests import framegen as G
+
+
+def _with_fcs(f: bytes) -> bytes:
+    return f + struct.pack("<I", O.crc32(f))
+
+
+def _case_frames(seed: int, count: int):
+    """Frames with FCS: valid ones, some with a flipped payload / FCS byte, short ones."""
+    rng = np.random.default_rng(seed)
+    out = []
+    base = G.frames(seed=seed, count=count)
+    for i, f in enumerate(base):
+        b = bytearray(_with_fcs(f))
+        r = rng.random()
+        if r < 0.15 and len(b) > 4:
+            b[rng.integers(0, len(b))] ^= 1 << int(rng.integers(0, 8))  # corrupt: FCS fails
+        elif r < 0.18:
+            b = b[: int(rng.integers(0, 4))]  # shorter than an FCS
+        out.append(bytes(b))
+    return out
+
+
+def _expect(frames):
+    ok = np.array([int(len(f) >= 4 and O.crc32(f) == L.CRC32_RESIDUE) for f in frames], dtype=np.uint8)
+    verdict = np.array([O.ingress_verdict(f[:-4] if len(f) >= 4 else b"") for f in frames], dtype=np.uint8)
+    return ok, verdict
+
+
+def _cap_for(frames, offset):
+    """Slot capacity: the largest buffer, rounded up to 4 bytes."""
+    return (max(len(f) for f in frames) + offset + 3) & ~3
+
+
+def test_ring_requires_a_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(L.LnetoError):
+        L.RxRing(16)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offset", [0, 2, 16])
+def test_ring_slots_ingress(cuda, offset):
+    frames = _case_frames(seed=11 + offset, count=1200)
+    cap = _cap_for(frames, offset)
+    ring = L.RxRing(len(frames) + 7, slot_cap=cap, batch_slots=256, depth=3)
+    try:
+        for i, f in enumerate(frames):
+            ring.slots[i + 7, :offset] = 0xEE  # headroom before the frame
+            ring.slots[i + 7, offset:offset + len(f)] = np.frombuffer(f, dtype=np.uint8)
+            ring.lengths[i + 7] = offset + len(f)
+        ok, verdict = ring.ingress(first=7, count=len(frames), offset=offset)
+        want_ok, want_v = _expect(frames)
+        assert np.array_equal(ok, want_ok)
+        bad = np.flatnonzero(verdict != want_v)
+        assert bad.size == 0, [(int(i), int(verdict[i]), int(want_v[i]), len(frames[i])) for i in bad[:20]]
+        assert want_ok.sum() > 900 and (want_ok == 0).sum() > 150
+    finally:
+        ring.close()
+
+
+@pytest.mark.gpu
+def test_ring_evil_bit_flag(cuda):
+    frames = _case_frames(seed=5, count=600)
+    ring = L.RxRing(len(frames), slot_cap=_cap_for(frames, 0), batch_slots=200, depth=2)
+    try:
+        ok, verdict = ring.ingress_packets(frames, offset=0, flags=L.VERIFY_EVIL_BIT)
+        want_v = np.array([O.ingress_verdict(f[:-4] if len(f) >= 4 else b"", O.VERIFY_EVIL_BIT) for f in frames],
+                          dtype=np.uint8)
+        assert np.array_equal(verdict, want_v)
+    finally:
+        ring.close()
+
+
+@pytest.mark.gpu
+def test_ingress_packets_gather(cuda):
+    """Caller-owned buffers, more frames than the ring has slots (several gather
+    rounds over the stages), empty buffers and full-capacity buffers."""
+    frames = _case_frames(seed=3, count=2500)
+    rng = np.random.default_rng(9)
+    offset = 4
+    cap = _cap_for(frames, offset)
+    frames += [b"", b"\x01\x02", bytes(rng.integers(0, 256, 1020, dtype=np.uint8))]
+    frames.append(_with_fcs(bytes(rng.integers(0, 256, cap - offset - 4, dtype=np.uint8))))  # fills the slot
+    bufs = [b"\xAA" * offset + f for f in frames]
+    assert max(len(b) for b in bufs) == cap
+    ring = L.RxRing(600, slot_cap=cap, batch_slots=100, depth=3)
+    try:
+        ok, verdict = ring.ingress_packets(bufs, offset=offset)
+    finally:
+        ring.close()
+    want_ok, want_v = _expect(frames)
+    assert np.array_equal(ok, want_ok)
+    assert np.array_equal(verdict, want_v)
+    assert ok[-1] == 1
+
+
+@pytest.mark.gpu
+def test_ingress_packets_rejects_oversize(cuda):
+    ring = L.RxRing(8, slot_cap=64)
+    try:
+        with pytest.raises(L.LnetoError):
+            ring.ingress_packets([b"x" * 65])
+    finally:
+        ring.close()
+
+
+@pytest.mark.gpu
+def test_ring_mtu_batch_roundtrip(cuda):
+    """64 Ki x 1500-byte frames with FCS through the pipelined ring: all pass;
+    then one flipped byte per 1000 frames fails exactly those frames."""
+    n, flen = 1 << 16, 1500
+    ring = L.RxRing(n, slot_cap=1536, batch_slots=8192, depth=3)
+    try:
+        rng = np.random.default_rng(1)
+        data = rng.integers(0, 256, (n, flen - 4), dtype=np.uint8)
+        ring.slots[:, : flen - 4] = data
+        crcs = np.array([O.crc32(r.tobytes()) for r in data[:256]], dtype=np.uint32)
+        # FCS for all rows via the device CRC of the same bytes
+        import torch
+        d = torch.from_numpy(data.reshape(-1)).to(cuda)
+        off = torch.arange(n + 1, dtype=torch.int64, device=cuda) * (flen - 4)
+        fcs = L.crc32_batch(d, off).cpu().numpy().view(np.uint32)
+        assert np.array_equal(fcs[:256], crcs)
+        ring.slots[:, flen - 4: flen] = fcs.view(np.uint8).reshape(n, 4)
+        ring.lengths[:] = flen
+        ok, _ = ring.ingress(0, n)
+        assert ok.all()
+        bad = np.arange(0, n, 1000)
+        ring.slots[bad, 77] ^= 0x10
+        ok, _ = ring.ingress(0, n)
+        assert np.array_equal(np.flatnonzero(ok == 0), bad)
+    finally:
+        ring.close()
