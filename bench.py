@@ -107,6 +107,46 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
     }
 
 
+def rx_ring_bench(args, L, synth, torch, dev, world):
+    """PCIe-inclusive receive path: frames
+    (1500 B incl. their LE FCS) sit in the ring's pinned host slots as a NIC
+    would leave them; one step = lnx_rx_ring_ingress over all of them: H2D,
+    FCS verify, receive-path verdicts, D2H, pipelined over --ring-depth HIP
+    streams.  Host wall clock per step; never the headline `value`."""
+    if world != 1:
+        raise SystemExit("--op rx_ring runs on one GPU")
+    n, flen, cap = 1 << 20, FRAME_BYTES, 1536
+    d = synth.bytes_torch(n * flen, dev).view(n, flen)
+    starts = torch.arange(n, dtype=torch.int64, device=dev) * flen
+    lens = torch.full((n,), flen - 4, dtype=torch.int32, device=dev)
+    fcs = L.crc32_segments(d.view(-1), starts, lens)
+    d[:, flen - 4:] = fcs.view(torch.uint8).view(n, 4)
+    ring = L.RxRing(n, slot_cap=cap, batch_slots=args.ring_batch, depth=args.ring_depth)
+    try:
+        torch.from_numpy(ring.slots)[:, :flen].copy_(d.cpu())
+        ring.lengths[:] = flen
+        del d
+        for _ in range(max(args.warmup, 1)):
+            ok, verdict = ring.ingress(0, n)
+        assert ok.all(), "FCS verify failed on valid frames"
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            ring.ingress(0, n)
+        el = (time.perf_counter() - t0) / args.steps
+    finally:
+        ring.close()
+    out = {
+        "metric": "GiB/s receive ring, PCIe-inclusive (pinned slots -> H2D -> FCS verify + ingress verdicts -> D2H)",
+        "value": round(n * flen / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic 1500-byte frames with valid FCS in 1536-byte slots",
+        "config": {"workload": "1M x 1500 B frames in host memory", "frames": n, "slot_cap": cap,
+                   "pcie_bytes_per_step": n * cap, "depth": args.ring_depth, "batch_slots": args.ring_batch,
+                   "kernel": L.version()},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,7 +154,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
-    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress"])
+    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress", "rx_ring"])
+    ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
+    ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
@@ -145,6 +187,9 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     cdev = torch.device("cpu") if share else dev  # device of the timing tensors
+
+    if args.op == "rx_ring":
+        return rx_ring_bench(args, L, synth, torch, dev, world)
 
     wname, n_rank, flen, desc = workload_spec(args.workload, world)
     # Frame index slice of this rank within the global batch (weak scaling:

@@ -187,3 +187,43 @@ inline int VerifyIngressBatch(const uint8_t* d_frames, const uint64_t* d_off, ui
   return lnx_ingress_verify_batch(d_frames, d_off, n, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, d_verdict, stream);
 }
 }  // namespace internet
+
+namespace netdev {
+// Receive ring: bufferSelect-style pinned slots
+// (x/netdev/buffer.go:25-37) whose batches run through FCS verify and the
+// receive-path verdicts on the GPU.  IngressPackets mirrors
+// netdev.Stack.IngressPackets(bufs [][]byte, offset int) (x/netdev/interface.go:82-89):
+// frame k = bufs[k][offset:], FCS included; per frame fcsOK and verdict.
+class RxRing {
+ public:
+  RxRing() = default;
+  RxRing(const RxRing&) = delete;
+  RxRing& operator=(const RxRing&) = delete;
+  ~RxRing() { lnx_rx_ring_destroy(r_); }
+  int Open(int device, uint32_t nslots, uint32_t slotCap, uint32_t batchSlots = 0, uint32_t depth = 3) {
+    lnx_rx_ring_destroy(r_);
+    r_ = nullptr;
+    nslots_ = nslots, cap_ = slotCap;
+    return lnx_rx_ring_create(device, nslots, slotCap, batchSlots, depth, &r_);
+  }
+  // Slot i's pinned buffer (slotCap bytes) and its length, for a producer.
+  uint8_t* Slot(uint32_t i) { return lnx_rx_ring_slots(r_) + size_t(i) * cap_; }
+  uint32_t& Len(uint32_t i) { return lnx_rx_ring_lengths(r_)[i]; }
+  // Slots [first, first + count) as IngressPackets(slots, offset).
+  int Ingress(uint32_t first, uint32_t count, uint32_t offset, uint8_t* fcsOK, uint8_t* verdict,
+              bool evilBit = false) {
+    return lnx_rx_ring_ingress(r_, first, count, offset, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, fcsOK, verdict);
+  }
+  // Caller-owned buffers (gathered into the slots).
+  int IngressPackets(const uint8_t* const* bufs, const uint32_t* lens, uint64_t n, uint32_t offset, uint8_t* fcsOK,
+                     uint8_t* verdict, bool evilBit = false) {
+    return lnx_ingress_packets(r_, bufs, lens, n, offset, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, fcsOK, verdict);
+  }
+  uint32_t Slots() const { return nslots_; }
+  uint32_t SlotCap() const { return cap_; }
+
+ private:
+  lnx_rx_ring* r_ = nullptr;
+  uint32_t nslots_ = 0, cap_ = 0;
+};
+}  // namespace netdev

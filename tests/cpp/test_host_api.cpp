@@ -106,7 +106,31 @@ static void TestAppendFCS() {
   EXPECT(ethernet::CRC32(lneto::Bytes(frame.data(), n)) == LNX_CRC32_RESIDUE, "residue");
 }
 
+// The receive ring through the C++ mirror: without a GPU it must refuse to
+// open (no silent CPU path); with one, a valid and a corrupted frame.
+static void TestRxRing() {
+  netdev::RxRing ring;
+  const int rc = ring.Open(0, 4, 256);
+  if (lnx_device_count() == 0) {
+    EXPECT(rc == LNX_ENODEV || rc == LNX_EHIP, "ring without a device: got %d", rc);
+    return;
+  }
+  EXPECT(rc == LNX_OK, "ring open: %d", rc);
+  uint8_t* f = ring.Slot(0);
+  for (int i = 0; i < 60; ++i) f[i] = uint8_t(i);
+  internet::StackEthernetConfig cfg;
+  cfg.CRC32Update = ethernet::CRC32Update;
+  ring.Len(0) = uint32_t(internet::AppendFCS(f, 60, cfg));
+  std::memcpy(ring.Slot(1), f, ring.Len(0));
+  ring.Slot(1)[5] ^= 1;
+  ring.Len(1) = ring.Len(0);
+  uint8_t ok[2] = {9, 9}, verdict[2];
+  EXPECT(ring.Ingress(0, 2, 0, ok, verdict) == LNX_OK, "ingress");
+  EXPECT(ok[0] == 1 && ok[1] == 0, "fcs ok %d %d", ok[0], ok[1]);
+}
+
 int main() {
+  TestRxRing();
   TestCRC32Search();
   TestIPv4TCPChecksum();
   TestAppendFCS();

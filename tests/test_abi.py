@@ -80,3 +80,9 @@ def test_rows_kernel_algebra_emulated_on_cpu(tmp_path):
                     "-llneto_amd", f"-Wl,-rpath,{os.path.dirname(L.LIB_PATH)}"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_host_api_on_gpu(cuda, tmp_path):
+    """The same C++ program on the MI355X: the ring opens and verifies FCS."""
+    test_cpp_host_api_compiles_and_runs(tmp_path)
