@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 import lneto_amd as L
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
