@@ -378,15 +378,25 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 
   uint32_t reg = 0;  // this lane's CRC register for its row's frame in progress
   int live = 0;      // slots holding work
-  // 4-lane rows hold their results in registers and write them RL at a time:
-  // lane p of a row holds the row's p-th finished frame (hf) and its result
-  // (hv); pc counts them.  That saves stores where a wave finishes up to 16
-  // frames per slot (short frames, VALU-bound: 3 % on the Zipf mix).  16-lane
-  // rows store every slot instead: their held flushes write 16-byte pieces of
-  // output lines at uncorrelated times, and the partial-line writebacks cost
-  // 3 % at 1500 B, more than the per-slot stores (variant 4 vs 0).
-  constexpr bool kHold = RL == 4 && VAR != 4;
+  // Results are held in registers: lane p of a row holds the row's p-th
+  // finished frame (hf) and its result (hv); pc counts them.  A store per
+  // slot trickles writes into the read stream, which costs HBM read rate
+  // (tools/ubench/cluster.hip: 6 % for 4 B per frame).
+  //  * 4-lane rows (up to 16 frames per wave per slot) flush when a row holds
+  //    RL results: a store per 4 frames per row (3 % on the Zipf mix).
+  //  * 16-lane rows flush at the first slot after each 2^kWinLog ticks
+  //    (41 us) of the global 100 MHz clock, or when a row is full.  The
+  //    workgroup's waves then write their pieces of each output line within
+  //    one slot of each other, so lines are written whole and the chip
+  //    writes in bursts (+2.4 % at 1500 B, +1.6 % at 9000 B).  Flushing when
+  //    full alone wrote 16-byte pieces of lines at uncorrelated times, and
+  //    the partial-line writebacks made it 3 % slower than per-slot stores.
+  // VAR 4: one store per slot (A/B); VAR 5: clock windows for 4-lane rows too.
+  constexpr bool kHold = VAR != 4;
+  constexpr bool kWinFlush = kHold && (RL == 16 || VAR == 5);
+  constexpr int kWinLog = 12;
   uint32_t hf = 0, hv = 0, pc = 0;
+  uint32_t win = kWinFlush ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog) : 0u;
   auto flush = [&]() {
     store_result<MODE>(out_rsrc, p < pc, hf, hv);
     pc = 0;
@@ -541,7 +551,13 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     } else {
       if (fin.last && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
       pc += fin.last ? 1u : 0u;
-      if (wave_any(pc == (uint32_t)RL)) flush();
+      bool fl = wave_any(pc == (uint32_t)RL);
+      if constexpr (kWinFlush) {
+        const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
+        fl = fl || (now != win && wave_any(pc != 0));
+        win = now;
+      }
+      if (fl) flush();
     }
   };
 
@@ -733,7 +749,8 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
       case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
-      case 4: LNX_LAUNCH(CrcMode::kCrc, 4); break;  // one result store per slot for 4-lane rows too
+      case 4: LNX_LAUNCH(CrcMode::kCrc, 4); break;  // one result store per slot (no holding)
+      case 5: LNX_LAUNCH(CrcMode::kCrc, 5); break;  // clock-window flushes for 4-lane rows too
       case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;  // forced 4-lane rows
