@@ -749,7 +749,6 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
       case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
-      case 4: LNX_LAUNCH(CrcMode::kCrc, 4); break;  // one result store per slot (no holding)
       case 5: LNX_LAUNCH(CrcMode::kCrc, 5); break;  // clock-window flushes for 4-lane rows too
       case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
