@@ -150,13 +150,15 @@ def rx_ring_bench(args, L, synth, torch, dev, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress", "rx_ring"])
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="untimed launches for this long before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
@@ -235,6 +237,14 @@ def main():
         else:
             L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
 
+    # The first few hundred microseconds of launches on an idle GPU run at
+    # ramping clocks (tools/prof/variants.py measured ~5 % slower kernels):
+    # keep the device busy for --prewarm-s before the W warmup steps.
+    t_pw = time.perf_counter()
+    while time.perf_counter() - t_pw < args.prewarm_s:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -282,6 +292,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "prewarm_s": args.prewarm_s,
         "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",

@@ -97,12 +97,14 @@ std::vector<uint32_t> compact_image(const std::vector<uint32_t>& full) {
   return c;
 }
 
-// Both compact images back to back: [RL = 16][RL = 4] (lds_layout.hpp image_index).
+// The compact images back to back: [RL = 16][RL = 4][RL = 32] (lds_layout.hpp image_index).
 const std::vector<uint32_t>& host_image() {
   static const std::vector<uint32_t> img = [] {
-    std::vector<uint32_t> all = compact_image(build_lds_image(16));
-    const std::vector<uint32_t> i4 = compact_image(build_lds_image(4));
-    all.insert(all.end(), i4.begin(), i4.end());
+    std::vector<uint32_t> all;
+    for (uint32_t rl : {16u, 4u, 32u}) {
+      const std::vector<uint32_t> im = compact_image(build_lds_image(rl));
+      all.insert(all.end(), im.begin(), im.end());
+    }
     return all;
   }();
   return img;

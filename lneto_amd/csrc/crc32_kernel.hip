@@ -104,24 +104,31 @@ __device__ __forceinline__ uint32_t dpp_xor(uint32_t v) {
 }
 constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E, kRowRor4 = 0x124, kRowRor8 = 0x128;
 
-// XOR over the RL lanes of each row; every lane gets its row's result.
+// XOR over the RL lanes of each row; every lane gets its row's result.  A
+// 32-lane row spans two 16-lane DPP rows: v_permlane16_swap of v with itself
+// pairs them (gfx950).
 template <int RL>
 __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
   v = dpp_xor<kQuadX1>(v);
   v = dpp_xor<kQuadX2>(v);
-  if constexpr (RL == 16) {
+  if constexpr (RL >= 16) {
     v = dpp_xor<kRowRor4>(v);
     v = dpp_xor<kRowRor8>(v);
+  }
+  if constexpr (RL == 32) {
+    const auto sw = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = sw[0] ^ sw[1];
   }
   return v;
 }
 
 // Z_{-t}(R) for a row-uniform R, the nibbles shared over the row (T region);
-// t = 0 is the identity: each lane then contributes its nibbles in place.
+// t = 0 is the identity: each lane then contributes its nibbles in place.  A
+// 32-lane row does it per 16-lane half, both halves alike (q = p & 7).
 template <int RL>
 __device__ __forceinline__ uint32_t t_fix(const char* lds, uint32_t R, uint32_t t, uint32_t p, uint32_t bt) {
   const uint32_t tb = bt + (((t - 1u) & 3u) << 11);  // entry (h, t, v) = 48h + 16(t-1) + v, stride 128 B
-  if constexpr (RL == 16) {
+  if constexpr (RL >= 16) {
     const uint32_t q = p & 7u;  // lanes p and p+8 cover the same nibble
     const uint32_t nib = (R >> (4 * q)) & 15u;
     const uint32_t a0 = lds_rd(lds, tb + (nib << 7));
@@ -161,14 +168,44 @@ __device__ __forceinline__ uint32_t ld_buf(uint32_t voff, __amdgpu_buffer_rsrc_t
   return r;
 }
 
-#define LNX_L(k) "buffer_load_dword %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "]" LNX_LD_POL "\n\t"
 #define LNX_O(k) [o##k] "=v"(o[k])
 #define LNX_I(k) [i##k] "i"(IMM0 + (k) * D)
 // N (1..6) loads from one VGPR offset at immediates IMM0, IMM0 + D, ...
-template <int IMM0, int N, int D>
+// NT: non-temporal policy.  Only rows that read whole 128-byte lines per
+// instruction gain from it (32-lane rows, tools/ubench/pattern3.hip: +10 %
+// over default-policy rows); 64-byte half lines lose 10-20 % with nt.
+template <int IMM0, int N, int D, bool NT>
 __device__ __forceinline__ void ld_run(uint32_t* o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
   static_assert(N >= 1 && N <= 6 && IMM0 + (N - 1) * D <= 4095, "run shape");
-  if constexpr (N == 6) {
+#define LNX_L(k) "buffer_load_dword %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "] nt\n\t"
+  if constexpr (!NT) {
+  } else if constexpr (N == 6) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3) LNX_L(4) LNX_L(5)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3), LNX_O(4), LNX_O(5)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3), LNX_I(4), LNX_I(5));
+  } else if constexpr (N == 5) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3) LNX_L(4)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3), LNX_O(4)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3), LNX_I(4));
+  } else if constexpr (N == 4) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3));
+  } else if constexpr (N == 3) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2)
+                 : LNX_O(0), LNX_O(1), LNX_O(2)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2));
+  } else if constexpr (N == 2) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1)
+                 : LNX_O(0), LNX_O(1)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1));
+  } else {
+    asm volatile("s_nop 4\n\t" LNX_L(0) : LNX_O(0) : [v] "v"(v), [r] "s"(rsrc), LNX_I(0));
+  }
+#undef LNX_L
+#define LNX_L(k) "buffer_load_dword %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "]" LNX_LD_POL "\n\t"
+  if constexpr (NT) {
+  } else if constexpr (N == 6) {
     asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3) LNX_L(4) LNX_L(5)
                  : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3), LNX_O(4), LNX_O(5)
                  : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3), LNX_I(4), LNX_I(5));
@@ -197,12 +234,12 @@ __device__ __forceinline__ void ld_run(uint32_t* o, uint32_t v, __amdgpu_buffer_
 #undef LNX_I
 
 // All KS step loads of an item: runs of up to six from the one base offset.
-template <int K0, int KS, int D>
+template <int K0, int KS, int D, bool NT>
 __device__ __forceinline__ void ld_item(uint32_t* w, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
   if constexpr (K0 < KS) {
     constexpr int N = KS - K0 < 6 ? KS - K0 : 6;
-    ld_run<K0 * D, N, D>(w + K0, v, rsrc);
-    ld_item<K0 + N, KS, D>(w, v, rsrc);
+    ld_run<K0 * D, N, D, NT>(w + K0, v, rsrc);
+    ld_item<K0 + N, KS, D, NT>(w, v, rsrc);
   }
 }
 
@@ -303,8 +340,18 @@ template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
-  constexpr uint32_t kSbLog = RL == 16 ? 6 : 4;
-  static_assert(RL == 4 || RL == 16, "row width");
+  constexpr uint32_t kSbLog = RL == 32 ? 7 : RL == 16 ? 6 : 4;
+  static_assert(RL == 4 || RL == 16 || RL == 32, "row width");
+  // 32-lane rows read whole 128-byte lines: the window runs between line
+  // boundaries (the range descriptor is line-aligned, cx.adj), the loads are
+  // non-temporal, t = 4a + b window bytes follow the frame end (a < 32), the
+  // lanes p >= 32 - a skip the frame's last step (their word there is all
+  // junk), lane 31 - a takes the U-image of its b junk bytes out, and the
+  // finish rotates the registers by a lanes before F (DESIGN.md §3.1,
+  // tests/cpp/rows_emulator.cpp crc32w).  Narrower rows: window end = frame
+  // end rounded up to 4 bytes, t = 0..3 on the last lane.
+  constexpr bool kLine = RL == 32;
+  constexpr uint32_t kEndAlign = kLine ? 128u : 4u;
   static_assert(S >= 1 && NR <= (uint32_t)CH && CH <= 64 && S * NR <= 64, "chunk and bounds window shape");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
   constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3;  // steps, junk, start + end
@@ -393,7 +440,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   //    the partial-line writebacks made it 3 % slower than per-slot stores.
   // VAR 4: one store per slot (A/B); VAR 5: clock windows for 4-lane rows too.
   constexpr bool kHold = VAR != 4;
-  constexpr bool kWinFlush = kHold && (RL == 16 || VAR == 5);
+  constexpr bool kWinFlush = kHold && (RL >= 16 || VAR == 5);
   constexpr int kWinLog = 12;
   uint32_t hf = 0, hv = 0, pc = 0;
   uint32_t win = kWinFlush ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog) : 0u;
@@ -421,7 +468,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         const uint32_t n = (int32_t)len > 0 ? len : 0u;  // end below start: empty frame
         const uint32_t re = e_lo - o0_lo + adj;
         rf = f;
-        rea = (re + 3u) & ~3u;
+        rea = (re + kEndAlign - 1u) & ~(kEndAlign - 1u);
         rt = rea - re;
         rn = n;
         rJ = n ? (n + rt + SB - 1) >> kSbLog : 0u;
@@ -446,13 +493,15 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     // lead-in before the workgroup's first byte: those words read 0)
     const uint32_t voff = alive ? rea - ((rJ - rj) << kSbLog) + (p << 2) : kOOB;
     const bool ends = alive && rj + ns == rJ && rJ != 0;
-    const uint32_t jv = ends && p == RL - 1 && rt != 0 ? rea - 4u : kOOB;
+    // the word holding the frame end, when junk bytes follow it in that word
+    const uint32_t jl = kLine ? 31u - (rt >> 2) : (uint32_t)RL - 1u;
+    const uint32_t jv = ends && p == jl && (rt & 3u) != 0 ? rea - SB + (p << 2) : kOOB;
     rj += ns;
     if constexpr (VAR == 2) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) w[s][k] = voff * 0x9E3779B1u + k;
     } else {
-      ld_item<0, KS, (int)SB>(w[s], voff, data_rsrc);
+      ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
     }
     jk[s] = ld_buf<0>(jv, data_rsrc);
     // 4. bounds of the next S*NR frames, for this slot's next issue
@@ -496,7 +545,14 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       if (x1 > 0 && p == 0) m1 = (uint32_t)((1ull << (8 * x1)) - 1);
       reg = 0;
     }
-    const bool full = !wave_any(!alive || ns != (uint32_t)KS);
+    // steps this lane folds: 32-lane rows' junk lanes skip the frame's last step
+    const uint32_t nsl = kLine && last && ns != 0 && p >= 32u - (t >> 2) ? ns - 1u : ns;
+    const bool full = !wave_any(!alive || nsl != (uint32_t)KS);
+    // 32-lane rows: a 1500-byte frame spans 12 or 13 lines and its junk lanes
+    // skip one, so a one-item frame's lanes fold KS - 2 .. KS steps: only the
+    // last kTail steps need predication
+    constexpr int kTail = kLine && KS > 2 ? 2 : KS;
+    const bool near = !full && !wave_any(!alive || nsl + (uint32_t)kTail < (uint32_t)KS);
     auto word = [&](int k) {
       uint32_t x = w[s][k];
       if (k == 0) x = (x & keep) ^ initm;
@@ -514,17 +570,27 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 #pragma unroll
         for (int k = 0; k < KS - 1; ++k) in = u_step_xor(lds, in, word(k + 1), bu0, bu1);
         reg = u_step_xor(lds, in, 0u, bu0, bu1);
+      } else if (kTail < KS && near) {
+        uint32_t in = reg ^ word(0);
+#pragma unroll
+        for (int k = 0; k < KS - kTail - 1; ++k) in = u_step_xor(lds, in, word(k + 1), bu0, bu1);
+        reg = u_step_xor(lds, in, 0u, bu0, bu1);
+#pragma unroll
+        for (int k = KS - kTail; k < KS; ++k) {
+          const uint32_t r2 = u_step_xor(lds, reg ^ word(k), 0u, bu0, bu1);
+          reg = (uint32_t)k < nsl ? r2 : reg;
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
           const uint32_t r2 = u_step_xor(lds, reg ^ word(k), 0u, bu0, bu1);
-          reg = (uint32_t)k < ns ? r2 : reg;
+          reg = (uint32_t)k < nsl ? r2 : reg;
         }
       }
     }
     Fin fin;
     fin.reg = reg;
-    fin.junk = jk[s] & ~(uint32_t)(0xFFFFFFFFull >> (8 * t));
+    fin.junk = jk[s] & ~(uint32_t)(0xFFFFFFFFull >> (8 * (t & 3u)));
     fin.f = it_f[s];
     fin.n = n;
     fin.t = t;
@@ -538,8 +604,12 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     if (fin.any) {
       // the last lane absorbed t junk bytes past the frame end: take their
       // U-image out (junk is 0 on every other lane, and U(0) = 0)
-      const uint32_t r = fin.reg ^ u_step(lds, fin.junk, bu0, bu1);
-      uint32_t R = t_fix<RL>(lds, row_xor<RL>(f_step(lds, r, bf)), t, p, bt);
+      uint32_t r = fin.reg ^ u_step(lds, fin.junk, bu0, bu1);
+      if constexpr (kLine) {  // lane q takes the register of lane q - a (mod 32) of its row
+        const uint32_t src = (row << 5) | ((p - (t >> 2)) & 31u);
+        r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)r);
+      }
+      uint32_t R = t_fix<RL>(lds, row_xor<RL>(f_step(lds, r, bf)), t & 3u, p, bt);
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
       crc = ~R;
@@ -592,10 +662,20 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 }
 
 // ------------------------------------------------------------------ kernel
-// Row width per workgroup from its frames' mean length (RLF = 0), or forced
-// (RLF = 4 / 16, profiling); item size, ring depth and chunk per row width.
-template <CrcMode MODE, int VAR = 0, int RLF = 0, int KS16 = 24, int S16 = 1, int KS4 = 12, int S4 = 2,
-          int CH16 = 4, int CH4 = 16, bool SEG = false>
+// Row width per workgroup from its frames' mean length (RLF = 0): 4-lane rows
+// below kShortMean, 32-lane rows from kLineMean on, 16-lane rows between; or
+// forced (RLF = 4 / 16 / 32, profiling).  Item size, ring depth and chunk:
+// KSW, SW, CHW for 32-lane rows (for 16-lane rows too when forced; auto mode
+// gives them 24, 1, 4), KS4, S4, CH4 for 4-lane rows.
+//
+// Why three widths: 32-lane rows read whole lines with nt loads and reach
+// 6.5-6.65 TB/s on 9000-byte frames, but they finish 2 frames per wave-slot
+// where 16-lane rows finish 4, and at 1500 bytes (one 13-line item per frame)
+// that per-frame work makes them VALU-bound (4.9 TB/s against 5.8 for
+// 16-lane rows).
+constexpr uint64_t kLineMean = 4096;
+template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 12, int S4 = 2,
+          int CHW = 4, int CH4 = 16, bool SEG = false>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -615,8 +695,12 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     return SEG ? (f1 > f0 ? off[f1 - 1] + seg_len[f1 - 1] : 0) : off[f1];
   };
   const uint64_t ob0 = lo_of(fb0, fb1), ob1 = hi_of(fb0, fb1);
-  bool narrow = RLF == 4;
-  if constexpr (RLF == 0) narrow = fb1 > fb0 && ob1 > ob0 && ob1 - ob0 < kShortMean * (fb1 - fb0);
+  int rl = RLF;
+  if constexpr (RLF == 0) {
+    const uint64_t nf_ = fb1 - fb0, nb_ = ob1 > ob0 ? ob1 - ob0 : 0;
+    rl = nf_ == 0 || nb_ < kShortMean * nf_ ? 4 : nb_ < kLineMean * nf_ ? 16 : 32;
+  }
+  const bool narrow = rl == 4;
   {
     // compact image (lds_layout.hpp): thread t expands U value t into its 32
     // bank replicas (128 contiguous bytes, eight 16-byte writes started at a
@@ -625,7 +709,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // the chunk counter at 0
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          (narrow ? image_index(4) : image_index(16)) * kCompactDwords;
+                          image_index(rl) * kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
     const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
@@ -661,7 +745,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   if (fb1 == fb0) return;
 
   // A range (a workgroup's slice of frames) is addressed through one buffer
-  // descriptor whose base is 4-byte aligned: rel(x) = x - off[fb0] + adj.
+  // descriptor whose base is 4-byte aligned (128-byte aligned for 32-lane
+  // rows, whose windows run between lines): rel(x) = x - off[fb0] + adj.
+  const uint32_t amask = rl == 32 ? 127u : 3u;
   struct Range {
     uint64_t f0, f1, o0, o1;
     bool fits;  // byte range within 31-bit buffer offsets
@@ -672,14 +758,14 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     r.f1 = r.f0 + per_block < nframes ? r.f0 + per_block : nframes;
     r.o0 = o0, r.o1 = o1;
     const uint64_t bytes_ = o1 > o0 ? o1 - o0 : 0;  // non-decreasing offsets are the contract
-    const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + o0) & 3u);
+    const uint32_t adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + o0) & amask);
     r.fits = bytes_ + adj + 4096 < (1ull << 31);
     return r;
   };
   auto ctx_of = [&](const Range& r) -> WaveCtx {
     WaveCtx cx;
     const uint64_t bytes_ = r.o1 > r.o0 ? r.o1 - r.o0 : 0;
-    cx.adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + r.o0) & 3u);
+    cx.adj = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + r.o0) & amask);
     cx.nfb = (uint32_t)(r.f1 - r.f0);
     cx.data_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + r.o0 - cx.adj), (short)0,
                                                      (int)((bytes_ + cx.adj + 3) & ~3ull), 0x00020000);
@@ -702,9 +788,12 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
-    } else {
+    } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
       rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
+    } else {
+      L.p = lane & 31u, L.row = lane >> 5;
+      rows_generic<MODE, 32>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
     }
   } else {
     // chunks of the own slice from the LDS counter
@@ -713,9 +802,12 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
-    } else {
+    } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, KS16, S16, CH16, VAR, SEG>(lds, L, cx);
+      rows_body<MODE, 16, RLF == 16 ? KSW : 24, RLF == 16 ? SW : 1, RLF == 16 ? CHW : 4, VAR, SEG>(lds, L, cx);
+    } else if (RLF != 16) {
+      L.p = lane & 31u, L.row = lane >> 5;
+      rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG>(lds, L, cx);
     }
   }
   if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
@@ -744,13 +836,22 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
     // profiling variants (tools/prof/variants.py).  Arguments:
-    // VAR, forced row width (0 = per workgroup), KS16, S16, KS4, S4, CH16, CH4
+    // VAR, forced row width (0 = per workgroup), KSW, SW, KS4, S4, CHW, CH4
     switch (var) {
+      // 10-16: forced 32-lane rows (KSW, SW, CHW vary); 17: forced 16-lane rows
+      case 10: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 1, 12, 2, 4, 16); break;  // one 13-line item per 1500 B
+      case 11: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 2, 12, 2, 4, 16); break;  // two-slot ring
+      case 12: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 14, 1, 12, 2, 4, 16); break;
+      case 13: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 1, 12, 2, 2, 16); break;  // 2-frame chunks
+      case 14: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 1, 12, 2, 8, 16); break;  // 8-frame chunks
+      case 15: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 24, 1, 12, 2, 4, 16); break;  // 24-line items
+      case 16: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 18, 1, 12, 2, 4, 16); break;
+      case 17: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16); break;
       case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
       case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
       case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
       case 5: LNX_LAUNCH(CrcMode::kCrc, 5); break;  // clock-window flushes for 4-lane rows too
-      case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16); break;  // forced 16-lane rows
+      case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16); break;  // forced 16-lane rows
       case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;  // forced 4-lane rows
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 8, 3, 4, 64); break;

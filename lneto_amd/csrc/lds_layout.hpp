@@ -46,7 +46,7 @@ constexpr uint32_t kLdsDwords = kLdsBytes / 4;
 constexpr uint32_t kFBase = 131072;                // start of the F region
 constexpr uint32_t kTBase = 147456;                // start of the T region
 constexpr uint32_t kCtrBase = 159744;              // frame-chunk counter (one dword)
-constexpr int kImageCount = 2;                     // images: [0] RL = 16, [1] RL = 4
+constexpr int kImageCount = 3;                     // images: [0] RL = 16, [1] RL = 4, [2] RL = 32
 
 constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
   return ((m >> 1) << 16) | (e << 8) | ((m & 1) << 7) | (c << 2);
@@ -58,7 +58,7 @@ constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // 
   return kTBase + ((48u * h + 16u * (t - 1) + v) << 7) + (c << 2);
 }
 static_assert(t_addr(31, 1, 3, 15) < kCtrBase, "T region overlaps the counter");
-constexpr int image_index(int rl) { return rl == 16 ? 0 : 1; }
+constexpr int image_index(int rl) { return rl == 16 ? 0 : rl == 4 ? 1 : 2; }
 
 // Compact image in HBM (what a workgroup reads at start): the 1024 distinct U
 // values U_m[e] at dword 256m + e, then the [kFBase, kLdsBytes) tail of the

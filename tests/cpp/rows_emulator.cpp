@@ -3,8 +3,10 @@
 // build_lds_image) at the byte addresses the kernel uses.  Checks the window
 // geometry (aligned window end, lead-in mask, init fold and its spill, junk
 // removal, F_p, row XOR, Z_{-t} fix) against a plain table CRC-32 for every
-// length 0..N at every start alignment and in every row of the wave, for both
-// row widths.  No GPU: this pins the algebra and the table contents on the CPU.
+// length 0..N at every start alignment and in every row of the wave, for all
+// three row widths (32-lane rows: line-aligned window, junk lanes skipping the
+// last step, register rotation before F).  No GPU: this pins the algebra and
+// the table contents on the CPU.
 // Built and run by tests/test_abi.py.
 #include <cstdint>
 #include <cstdio>
@@ -48,6 +50,52 @@ struct Emu {
   static uint32_t keep_from(int32_t lo) {
     lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
     return (uint32_t)(0xFFFFFFFFull << (8 * lo));
+  }
+  // 32-lane rows (crc32_kernel.hip rows_body, RL = 32): the window runs from
+  // the 128-byte line holding the frame start to the end of the line holding
+  // its last byte, so every step reads one whole line.  t = 4a + b window bytes
+  // follow the frame end: lanes p >= 32 - a hold only those in the last step
+  // and skip it, lane 31 - a (when b > 0) takes the U-image of its b junk bytes
+  // out, and the registers are rotated by a lanes so that lane q's own F_q
+  // lands every one of them on the frame end less b bytes; Z_{-b} finishes.
+  uint32_t crc32w(const std::vector<uint8_t>& buf, uint32_t rs, uint32_t re) const {
+    const uint32_t SB = 128;
+    const uint32_t n = re > rs ? re - rs : 0;
+    const uint32_t ea = (re + SB - 1) & ~(SB - 1), t = ea - re, a = t >> 2, b = t & 3;
+    const uint32_t J = n ? (n + t + SB - 1) / SB : 0;
+    const int64_t ws = (int64_t)ea - (int64_t)J * SB;
+    const uint32_t lead = J * SB - n - t;
+    std::vector<uint32_t> lanes(32);
+    for (uint32_t p = 0; p < 32; ++p) {
+      const uint32_t m4 = n < 4 ? n : 4;
+      const int32_t d0 = (int32_t)lead - (int32_t)(4 * p);
+      const uint32_t keep = keep_from(d0), initm = keep & ~keep_from(d0 + (int32_t)m4);
+      const int32_t x1 = (int32_t)(lead + m4) - (int32_t)SB;
+      const uint32_t m1 = (x1 > 0 && p == 0) ? (uint32_t)((1ull << (8 * x1)) - 1) : 0;
+      const uint32_t Jp = (J && p >= 32 - a) ? J - 1 : J;
+      uint32_t reg = 0;
+      for (uint32_t j = 0; j < Jp; ++j) {
+        uint32_t x = word(buf, ws + 4 * p + (int64_t)SB * j);
+        if (j == 0) x = (x & keep) ^ initm;
+        if (j == 1) x ^= m1;
+        reg = U(reg ^ x, p);
+      }
+      if (J && b && p == 31 - a) {
+        const uint32_t junk = word(buf, (int64_t)ea - SB + 4 * p) & ~(uint32_t)(0xFFFFFFFFull >> (8 * b));
+        reg ^= U(junk, p);
+      }
+      lanes[p] = reg;
+    }
+    uint32_t R = 0;
+    for (uint32_t q = 0; q < 32; ++q) R ^= F(lanes[(q - a) & 31], q);  // rotation, F_q, row_xor
+    uint32_t T = 0;
+    for (uint32_t p = 0; p < 8; ++p) {
+      const uint32_t nib = (R >> (4 * p)) & 15;
+      T ^= b ? rd(t_addr(p, 0, b, nib)) : nib << (4 * p);
+    }
+    R = n ? T : 0;
+    if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    return ~R;
   }
   // CRC of frame [rs, re) of buf as row `row` of a wave would compute it.
   uint32_t crc(const std::vector<uint8_t>& buf, uint32_t rs, uint32_t re, uint32_t row) const {
@@ -116,14 +164,14 @@ int main() {
     b = (uint8_t)(s >> 56);
   }
   int bad = 0, checked = 0;
-  for (int rl : {16, 4}) {
+  for (int rl : {32, 16, 4}) {
     Emu e{rl, build_lds_image((uint32_t)rl)};
     const uint32_t nr = 64 / rl;
     for (uint32_t n = 0; n <= 1100; ++n) {
-      for (uint32_t start : {0u, 1u, 2u, 3u, 61u, 130u, 4093u}) {
+      for (uint32_t start : {0u, 1u, 2u, 3u, 61u, 124u, 125u, 127u, 128u, 130u, 4093u}) {
         if (start + n > buf.size()) continue;
         const uint32_t row = (n + start) % nr;
-        const uint32_t got = e.crc(buf, start, start + n, row);
+        const uint32_t got = rl == 32 ? e.crc32w(buf, start, start + n) : e.crc(buf, start, start + n, row);
         const uint32_t want = ref_crc(&buf[start], n);
         ++checked;
         if (got != want && bad++ < 10)

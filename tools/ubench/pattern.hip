@@ -17,7 +17,7 @@ __device__ inline uint32_t fold(uint32_t v) { return v; }
 __device__ inline uint32_t fold(uint2 v) { return v.x ^ v.y; }
 __device__ inline uint32_t fold(uint4 v) { return v.x ^ v.y ^ v.z ^ v.w; }
 
-template <int W, int ROWS, int U>
+template <int W, int ROWS, int U, bool NT = false>
 __global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, uint64_t nframes, uint32_t fb,
                                             uint64_t fpw, uint32_t* out) {
   typedef typename V<W>::T T;
@@ -34,7 +34,17 @@ __global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, ui
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         uint32_t oo = o + u * rowbytes + p * W;
-        v[u] = oo + W <= fb ? *(const T*)(fr + oo) : T{};
+        if constexpr (NT) {
+          typedef uint32_t vw __attribute__((ext_vector_type(W / 4)));
+          if (oo + W <= fb) {
+            const vw t = __builtin_nontemporal_load((const vw*)(fr + oo));
+            __builtin_memcpy(&v[u], &t, W);
+          } else {
+            v[u] = T{};
+          }
+        } else {
+          v[u] = oo + W <= fb ? *(const T*)(fr + oo) : T{};
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) acc ^= fold(v[u]);
@@ -48,7 +58,8 @@ __global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, ui
 template <typename F>
 float tm(F fn) {
   hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
-  fn(); (void)hipDeviceSynchronize();
+  for (int i = 0; i < 100; ++i) fn();
+  (void)hipDeviceSynchronize();
   std::vector<float> t;
   for (int r = 0; r < 7; ++r) { (void)hipEventRecord(a); fn(); (void)hipEventRecord(b); (void)hipEventSynchronize(b);
     float ms; (void)hipEventElapsedTime(&ms, a, b); t.push_back(ms); }
@@ -63,8 +74,18 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&buf, nframes * fb); (void)hipMalloc(&out, 64);
   (void)hipMemset(buf, 3, nframes * fb);
   const uint64_t waves = 256 * 16, fpw = (nframes + waves - 1) / waves;
-#define RUN(W, R, U) { float ms = tm([&] { pat<W, R, U><<<256, 1024>>>(buf, nframes, fb, fpw, out); }); \
-  printf("W=%2d rows=%d unroll=%d rowbytes/load=%4d : %.3f ms %.1f GB/s\n", W, R, U, 64 / R * W, ms, nframes * fb / ms / 1e6); }
+#define RUNP(W, R, U, NT) { float ms = tm([&] { pat<W, R, U, NT><<<256, 1024>>>(buf, nframes, fb, fpw, out); }); \
+  printf("W=%2d rows=%d unroll=%d rowbytes/load=%4d%s : %.3f ms %.1f GB/s\n", W, R, U, 64 / R * W, NT ? " nt" : "", ms, nframes * fb / ms / 1e6); }
+#define RUN(W, R, U) RUNP(W, R, U, false)
+  if (argc > 2) {  // nt sweep
+    RUNP(4, 4, 12, false); RUNP(4, 4, 12, true); RUNP(4, 4, 24, true);
+    RUNP(4, 2, 12, false); RUNP(4, 2, 12, true); RUNP(4, 2, 6, true);
+    RUNP(4, 1, 6, true); RUNP(4, 1, 12, true);
+    RUNP(8, 4, 6, true); RUNP(8, 4, 12, true); RUNP(16, 4, 3, true); RUNP(16, 4, 6, true);
+    RUNP(16, 2, 3, true); RUNP(16, 1, 2, true);
+    RUNP(4, 16, 8, true); RUNP(8, 16, 4, true); RUNP(16, 16, 2, true); RUNP(16, 8, 2, true);
+    return 0;
+  }
   RUN(4, 4, 6); RUN(4, 4, 12); RUN(4, 4, 24);
   RUN(8, 4, 6); RUN(8, 4, 12);
   RUN(16, 4, 3); RUN(16, 4, 6);

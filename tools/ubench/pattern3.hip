@@ -1,0 +1,175 @@
+// Pipelined read ceiling of candidate CRC-kernel access shapes on PACKED
+// frames (1 M x 1500 B by default, 4-byte aligned starts like configs[1]).
+// Unlike pattern2.hip there is no drain per frame: each row walks the
+// windows of its frames (row r of a wave: frames f0 + r, f0 + r + rows, ...)
+// as one step sequence and keeps D loads in flight, like the product ring.
+// Window of a frame: [start & ~(A-1), end), RL*W bytes per step.  GB/s is
+// over the frames' bytes.  Policy bits (gfx950 cpol): sc0 = 1, nt = 2, sc1 = 16.
+// Not part of the product.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int W, int P>
+__device__ __forceinline__ uint32_t ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (W == 4) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, P);
+  } else if constexpr (W == 8) {
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, P);
+    return v[0] ^ v[1];
+  } else {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, P);
+    return v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+}
+template <int W>
+struct Vt;
+template <>
+struct Vt<4> {
+  typedef uint32_t T;
+};
+template <>
+struct Vt<8> {
+  typedef u32x2 T;
+};
+template <>
+struct Vt<16> {
+  typedef u32x4 T;
+};
+template <int W, int P>
+__device__ __forceinline__ typename Vt<W>::T ldv(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, P);
+  if constexpr (W == 8) return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, P);
+  if constexpr (W == 16) return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, P);
+}
+__device__ __forceinline__ uint32_t fold(uint32_t v) { return v; }
+__device__ __forceinline__ uint32_t fold(u32x2 v) { return v[0] ^ v[1]; }
+__device__ __forceinline__ uint32_t fold(u32x4 v) { return v[0] ^ v[1] ^ v[2] ^ v[3]; }
+
+template <int W, int RL, int D, int A, int P, bool RELOAD = false>
+__global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, uint32_t nbytes, uint32_t nframes,
+                                            uint32_t fb, uint32_t fpw, uint32_t* out) {
+  __shared__ uint32_t pad[40960];
+  constexpr uint32_t ROWS = 64 / RL, RB = RL * W;
+  const uint32_t lane = threadIdx.x & 63, p = lane % RL, row = lane / RL;
+  const uint32_t gw = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint32_t f0 = std::min(gw * fpw, nframes), f1 = std::min(f0 + fpw, nframes);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  // row state: frame f, next step address a, window end e
+  uint32_t f = f0 + row;
+  auto win = [&](uint32_t ff, uint32_t& a, uint32_t& e) {
+    if (ff < f1) {
+      a = (ff * fb) & ~(uint32_t)(A - 1);
+      e = ff * fb + fb;
+    } else {
+      a = 0x80000000u;
+      e = 0;
+    }
+  };
+  uint32_t a, e;
+  win(f, a, e);
+  uint32_t jo = 0x80000000u;  // RELOAD: this lane's word of the step that just ended a frame
+  auto next = [&]() -> uint32_t {  // address of this lane's next load, advance the row
+    const uint32_t o = a + p * W;
+    a += RB;
+    jo = 0x80000000u;
+    if (a >= e && f < f1) {
+      jo = o - p * W + p * 4;
+      f += ROWS;
+      win(f, a, e);
+    }
+    return o;
+  };
+  typename Vt<W>::T v[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) v[u] = ldv<W, P>(r, next());
+  uint32_t acc = 0;
+  for (;;) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      acc ^= fold(v[u]);
+      v[u] = ldv<W, P>(r, next());
+      if constexpr (RELOAD) acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, jo, 0, P);
+    }
+    if (!__builtin_amdgcn_ballot_w64(f < f1)) break;
+  }
+#pragma unroll
+  for (int u = 0; u < D; ++u) acc ^= fold(v[u]);
+  pad[threadIdx.x] = acc;
+  __syncthreads();
+  if (pad[(threadIdx.x + 1) & 1023] == 0x12345678u) out[0] = acc;
+}
+
+template <typename F>
+float tm(F fn) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int i = 0; i < 100; ++i) fn();
+  (void)hipDeviceSynchronize();
+  std::vector<float> t;
+  for (int r = 0; r < 9; ++r) {
+    (void)hipEventRecord(a);
+    fn();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    t.push_back(ms);
+  }
+  std::sort(t.begin(), t.end());
+  return t[4];
+}
+
+int main(int argc, char** argv) {
+  const uint32_t fb = argc > 1 ? (uint32_t)atoi(argv[1]) : 1500;
+  const uint32_t nframes = (uint32_t)std::min<uint64_t>(1048576, 2000000000ull / fb);
+  const uint32_t nbytes = nframes * fb;
+  uint8_t* buf;
+  uint32_t* out;
+  (void)hipMalloc(&buf, nbytes);
+  (void)hipMalloc(&out, 64);
+  (void)hipMemset(buf, 3, nbytes);
+  const uint32_t waves = 256 * 16, fpw = (nframes + waves - 1) / waves;
+#define RUNR(W, RL, D, A, P, RE)                                                                                     \
+  {                                                                                                             \
+    float ms = tm([&] { pat<W, RL, D, A, P, RE><<<256, 1024>>>(buf, nbytes, nframes, fb, fpw, out); });           \
+    printf("W=%2d RL=%2d D=%2d align=%3d pol=%2d%s : %.4f ms %.1f GB/s\n", W, RL, D, A, P, RE ? " reload" : "", ms, nbytes / ms / 1e6); \
+  }
+#define RUN(W, RL, D, A, P) RUNR(W, RL, D, A, P, false)
+  printf("frames %u x %u B\n", nframes, fb);
+  RUN(4, 16, 16, 64, 0);
+  RUNR(4, 32, 16, 128, 2, true);
+  RUNR(4, 32, 12, 128, 2, true);
+  RUNR(4, 32, 24, 128, 2, true);
+  RUNR(4, 32, 16, 128, 18, true);
+  RUNR(4, 32, 16, 128, 0, true);
+  RUN(4, 32, 12, 128, 2);
+  RUN(4, 32, 24, 128, 2);
+  RUN(4, 16, 16, 64, 2);
+  RUN(4, 32, 16, 128, 0);
+  RUN(4, 32, 16, 128, 2);
+  RUN(8, 16, 8, 128, 0);
+  RUN(8, 16, 8, 128, 2);
+  RUN(16, 16, 4, 256, 0);
+  RUN(16, 16, 4, 256, 2);
+  RUN(16, 16, 6, 256, 2);
+  RUN(16, 16, 8, 256, 2);
+  RUN(16, 16, 6, 128, 2);
+  RUN(16, 16, 6, 64, 2);
+  RUN(16, 16, 6, 16, 2);
+  RUN(16, 32, 4, 512, 2);
+  RUN(16, 32, 4, 128, 2);
+  RUN(16, 64, 4, 1024, 2);
+  RUN(16, 64, 4, 128, 2);
+  RUN(16, 16, 6, 128, 0);
+  RUN(16, 16, 6, 128, 16);
+  RUN(16, 16, 6, 128, 18);
+  return 0;
+}
