@@ -87,20 +87,23 @@ __device__ __forceinline__ uint32_t u_step_xor(const char* lds, uint32_t x, uint
   return __builtin_amdgcn_bitop3_b32(t, lds_rd(lds, a3 + 128), y, 0x96);
 }
 
-// F_p(r) through eight lane-private nibble tables.
+// F_p(r) through eight lane-private nibble tables: per nibble one v_bfe and
+// one v_lshl_add for the address (the table offset rides in the ds_read
+// immediate), the eight values XOR-ed by three v_bitop3 and a v_xor.
 __device__ __forceinline__ uint32_t f_step(const char* lds, uint32_t r, uint32_t bf) {
-  uint32_t acc = 0;
+  uint32_t v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t a = (((r >> (4 * i)) & 15u) << 7) | bf;
-    acc ^= lds_rd(lds, a + (uint32_t)(i << 11));
-  }
-  return acc;
+  for (int i = 0; i < 8; ++i) v[i] = lds_rd(lds, (__builtin_amdgcn_ubfe(r, 4 * i, 4) << 7) + bf + (uint32_t)(i << 11));
+  const uint32_t x = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
+  const uint32_t y = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
+  return __builtin_amdgcn_bitop3_b32(x, y, v[6] ^ v[7], 0x96);
 }
 
+// v ^ (v moved by the DPP control): bound_ctrl lets hipcc fold the move into
+// one v_xor_b32_dpp (no lane reads out of bounds with these controls).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_xor(uint32_t v) {
-  return v ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+  return v ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 constexpr int kQuadX1 = 0xB1, kQuadX2 = 0x4E, kRowRor4 = 0x124, kRowRor8 = 0x128;
 
@@ -243,10 +246,53 @@ __device__ __forceinline__ void ld_item(uint32_t* w, uint32_t v, __amdgpu_buffer
   }
 }
 
+// The same with dwordx2 loads (two words per lane; always non-temporal).
+#define LNX_L(k) "buffer_load_dwordx2 %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "] nt\n\t"
+#define LNX_O(k) [o##k] "=v"(o[k])
+#define LNX_I(k) [i##k] "i"(IMM0 + (k) * D)
+template <int IMM0, int N, int D>
+__device__ __forceinline__ void ld_run2(uint64_t* o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
+  static_assert(N >= 1 && N <= 6 && IMM0 + (N - 1) * D <= 4095, "run shape");
+  if constexpr (N == 6) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3) LNX_L(4) LNX_L(5)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3), LNX_O(4), LNX_O(5)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3), LNX_I(4), LNX_I(5));
+  } else if constexpr (N == 5) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3) LNX_L(4)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3), LNX_O(4)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3), LNX_I(4));
+  } else if constexpr (N == 4) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3));
+  } else if constexpr (N == 3) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2)
+                 : LNX_O(0), LNX_O(1), LNX_O(2)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2));
+  } else if constexpr (N == 2) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1)
+                 : LNX_O(0), LNX_O(1)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1));
+  } else {
+    asm volatile("s_nop 4\n\t" LNX_L(0) : LNX_O(0) : [v] "v"(v), [r] "s"(rsrc), LNX_I(0));
+  }
+}
+#undef LNX_L
+#undef LNX_O
+#undef LNX_I
+template <int K0, int KS, int D, bool NT>
+__device__ __forceinline__ void ld_item(uint64_t* w, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
+  if constexpr (K0 < KS) {
+    constexpr int N = KS - K0 < 6 ? KS - K0 : 6;
+    ld_run2<K0 * D, N, D>(w + K0, v, rsrc);
+    ld_item<K0 + N, KS, D, NT>(w, v, rsrc);
+  }
+}
+
 // vmcnt wait naming every register of one slot: the wait, then empty asm
 // statements that "redefine" each register, so no use is scheduled above it.
-template <int N, int KS>
-__device__ __forceinline__ void slot_wait(uint32_t (&w)[KS], uint32_t& junk, uint32_t& b0, uint32_t& b1) {
+template <int N, int KS, typename Word>
+__device__ __forceinline__ void slot_wait(Word (&w)[KS], uint32_t& junk, uint32_t& b0, uint32_t& b1) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N));
 #pragma unroll
   for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(w[k]));
@@ -336,21 +382,32 @@ struct WaveCtx {
 // sees its chunks as one virtual frame sequence v = 0, 1, ...: it holds the
 // bases of the chunk v is in (bc) and of the next one (bn), which covers the
 // S*NR-frame bounds window every slot prefetches.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG>
+//
+// WL: words per lane per step.  WL = 2 (16-lane rows only): each lane loads
+// two consecutive dwords (buffer_load_dwordx2), so a row reads a whole
+// 128-byte line per instruction like a 32-lane row, while a wave still
+// carries four frames.  Lane p then holds the registers of "virtual lanes"
+// v = 2p and 2p + 1 of a 32-virtual-lane row; all the window algebra below is
+// in virtual lanes.
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG, int WL = 1>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
-  constexpr uint32_t SB = 4 * RL;   // bytes a row consumes per step
-  constexpr uint32_t kSbLog = RL == 32 ? 7 : RL == 16 ? 6 : 4;
+  constexpr uint32_t VL = RL * WL;  // virtual lanes per row
+  constexpr uint32_t SB = 4 * VL;   // bytes a row consumes per step
+  constexpr uint32_t kSbLog = VL == 32 ? 7 : VL == 16 ? 6 : 4;
   static_assert(RL == 4 || RL == 16 || RL == 32, "row width");
-  // 32-lane rows read whole 128-byte lines: the window runs between line
-  // boundaries (the range descriptor is line-aligned, cx.adj), the loads are
-  // non-temporal, t = 4a + b window bytes follow the frame end (a < 32), the
-  // lanes p >= 32 - a skip the frame's last step (their word there is all
-  // junk), lane 31 - a takes the U-image of its b junk bytes out, and the
-  // finish rotates the registers by a lanes before F (DESIGN.md §3.1,
-  // tests/cpp/rows_emulator.cpp crc32w).  Narrower rows: window end = frame
-  // end rounded up to 4 bytes, t = 0..3 on the last lane.
-  constexpr bool kLine = RL == 32;
+  static_assert(WL == 1 || (WL == 2 && RL == 16), "two words per lane: 16-lane rows");
+  using Word = std::conditional_t<WL == 2, uint64_t, uint32_t>;
+  // Rows of 32 virtual lanes read whole 128-byte lines: the window runs
+  // between line boundaries (the range descriptor is line-aligned, cx.adj),
+  // the loads are non-temporal, t = 4a + b window bytes follow the frame end
+  // (a < 32), the virtual lanes v >= 32 - a skip the frame's last step (their
+  // word there is all junk), virtual lane 31 - a takes the U-image of its b
+  // junk bytes out, and the finish rotates the registers by a virtual lanes
+  // before F (tests/cpp/rows_emulator.cpp crc32w).  Narrower
+  // rows: window end = frame end rounded up to 4 bytes, t = 0..3 on the last
+  // lane.
+  constexpr bool kLine = VL == 32;
   constexpr uint32_t kEndAlign = kLine ? 128u : 4u;
   static_assert(S >= 1 && NR <= (uint32_t)CH && CH <= 64 && S * NR <= 64, "chunk and bounds window shape");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
@@ -396,8 +453,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   uint32_t nf = 0;          // next unassigned virtual frame of the wave (uniform)
 
   // ---- ring slots
-  uint32_t w[S][KS];
-  uint32_t jk[S];             // the last lane's last word (junk bytes past the frame end)
+  Word w[S][KS];
+  uint32_t jk[S];             // the word holding the frame end (junk bytes past it)
   uint32_t fi[S], sb[S], eb[S];  // lane i: frame of virtual index nfv[s] + i, its start / end (low dwords)
   uint32_t nfv[S];            // uniform
   uint32_t it_f[S], it_n[S], it_t[S], it_j0[S], it_ns[S];
@@ -423,7 +480,9 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     for (int s = 0; s < S; ++s) fi[s] = f, sb[s] = a, eb[s] = b;
   }
 
-  uint32_t reg = 0;  // this lane's CRC register for its row's frame in progress
+  uint32_t reg[WL];  // this lane's CRC registers (one per virtual lane) for its row's frame in progress
+#pragma unroll
+  for (int h = 0; h < WL; ++h) reg[h] = 0;
   int live = 0;      // slots holding work
   // Results are held in registers: lane p of a row holds the row's p-th
   // finished frame (hf) and its result (hv); pc counts them.  A store per
@@ -491,15 +550,15 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     hw[s] = wave_any(alive);
     // 3. streaming loads: w[k] = step rj + k from one base (negative for a
     // lead-in before the workgroup's first byte: those words read 0)
-    const uint32_t voff = alive ? rea - ((rJ - rj) << kSbLog) + (p << 2) : kOOB;
+    const uint32_t voff = alive ? rea - ((rJ - rj) << kSbLog) + p * 4u * WL : kOOB;
     const bool ends = alive && rj + ns == rJ && rJ != 0;
-    // the word holding the frame end, when junk bytes follow it in that word
-    const uint32_t jl = kLine ? 31u - (rt >> 2) : (uint32_t)RL - 1u;
-    const uint32_t jv = ends && p == jl && (rt & 3u) != 0 ? rea - SB + (p << 2) : kOOB;
+    // the (virtual) lane whose word holds the frame end, when junk bytes follow it in that word
+    const uint32_t jl = kLine ? 31u - (rt >> 2) : VL - 1u;
+    const uint32_t jv = ends && p == jl / WL && (rt & 3u) != 0 ? rea - SB + (jl << 2) : kOOB;
     rj += ns;
     if constexpr (VAR == 2) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) w[s][k] = voff * 0x9E3779B1u + k;
+      for (int k = 0; k < KS; ++k) w[s][k] = (Word)(voff * 0x9E3779B1u + k) * 0x100000001ull;
     } else {
       ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
     }
@@ -523,7 +582,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   // (F_p, row XOR, Z_{-t}, store) runs after the slot's next loads are out,
   // so its LDS round trips overlap them instead of idling the wave.
   struct Fin {
-    uint32_t reg, junk, f, n, t;
+    uint32_t reg[WL];
+    uint32_t junk, f, n, t;
     bool last, any;
   };
   auto compute = [&](auto sc) -> Fin {
@@ -534,62 +594,92 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     const bool alive = it_f[s] != kNoFrame;
     const bool first = alive && j0 == 0 && ns != 0;
     const bool last = alive && j0 + ns == J;
-    uint32_t keep = 0xFFFFFFFFu, initm = 0, m1 = 0;
+    uint32_t keep[WL], initm[WL], m1 = 0;
+#pragma unroll
+    for (int h = 0; h < WL; ++h) keep[h] = 0xFFFFFFFFu, initm[h] = 0;
     if (first) {
       const uint32_t lead = (J << kSbLog) - n - t;
       const uint32_t m4 = n < 4 ? n : 4u;
-      const int32_t d0 = (int32_t)lead - (int32_t)(p << 2);
-      keep = keep_from(d0);
-      initm = keep & ~keep_from(d0 + (int32_t)m4);
+#pragma unroll
+      for (int h = 0; h < WL; ++h) {
+        const int32_t d0 = (int32_t)lead - (int32_t)((p * WL + h) << 2);
+        keep[h] = keep_from(d0);
+        initm[h] = keep[h] & ~keep_from(d0 + (int32_t)m4);
+        reg[h] = 0;
+      }
       const int32_t x1 = (int32_t)(lead + m4) - (int32_t)SB;  // init bytes spilling into step 1
       if (x1 > 0 && p == 0) m1 = (uint32_t)((1ull << (8 * x1)) - 1);
-      reg = 0;
     }
-    // steps this lane folds: 32-lane rows' junk lanes skip the frame's last step
-    const uint32_t nsl = kLine && last && ns != 0 && p >= 32u - (t >> 2) ? ns - 1u : ns;
-    const bool full = !wave_any(!alive || nsl != (uint32_t)KS);
-    // 32-lane rows: a 1500-byte frame spans 12 or 13 lines and its junk lanes
-    // skip one, so a one-item frame's lanes fold KS - 2 .. KS steps: only the
-    // last kTail steps need predication
+    // steps each virtual lane folds: with line windows the junk lanes skip the
+    // frame's last step
+    uint32_t nsl[WL];
+    bool all_full = true, all_near = true;
+    // a 1500-byte frame spans 12 or 13 lines and its junk lanes skip one, so
+    // a one-item frame's lanes fold KS - 2 .. KS steps: only the last kTail
+    // steps need predication
     constexpr int kTail = kLine && KS > 2 ? 2 : KS;
-    const bool near = !full && !wave_any(!alive || nsl + (uint32_t)kTail < (uint32_t)KS);
-    auto word = [&](int k) {
-      uint32_t x = w[s][k];
-      if (k == 0) x = (x & keep) ^ initm;
-      if (k == 1) x ^= m1;
+#pragma unroll
+    for (int h = 0; h < WL; ++h) {
+      nsl[h] = kLine && last && ns != 0 && p * WL + h >= 32u - (t >> 2) ? ns - 1u : ns;
+      all_full = all_full && alive && nsl[h] == (uint32_t)KS;
+      all_near = all_near && alive && nsl[h] + (uint32_t)kTail >= (uint32_t)KS;
+    }
+    const bool full = !wave_any(!all_full);
+    const bool near = !full && !wave_any(!all_near);
+    auto word = [&](int k, int h) -> uint32_t {
+      uint32_t x = (uint32_t)(w[s][k] >> (32 * h));
+      if (k == 0) x = (x & keep[h]) ^ initm[h];
+      if (k == 1 && h == 0) x ^= m1;
       return x;
     };
     if constexpr (VAR == 1) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) reg ^= w[s][k];
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int h = 0; h < WL; ++h) reg[h] ^= word(k, h);
     } else {
       if (full) {
         // hot path: every row folds KS steps, no predication; the next word is
         // XOR-ed in by the step's second bitop3
-        uint32_t in = reg ^ word(0);
+        uint32_t in[WL];
 #pragma unroll
-        for (int k = 0; k < KS - 1; ++k) in = u_step_xor(lds, in, word(k + 1), bu0, bu1);
-        reg = u_step_xor(lds, in, 0u, bu0, bu1);
+        for (int h = 0; h < WL; ++h) in[h] = reg[h] ^ word(0, h);
+#pragma unroll
+        for (int k = 0; k < KS - 1; ++k)
+#pragma unroll
+          for (int h = 0; h < WL; ++h) in[h] = u_step_xor(lds, in[h], word(k + 1, h), bu0, bu1);
+#pragma unroll
+        for (int h = 0; h < WL; ++h) reg[h] = u_step_xor(lds, in[h], 0u, bu0, bu1);
       } else if (kTail < KS && near) {
-        uint32_t in = reg ^ word(0);
+        uint32_t in[WL];
 #pragma unroll
-        for (int k = 0; k < KS - kTail - 1; ++k) in = u_step_xor(lds, in, word(k + 1), bu0, bu1);
-        reg = u_step_xor(lds, in, 0u, bu0, bu1);
+        for (int h = 0; h < WL; ++h) in[h] = reg[h] ^ word(0, h);
 #pragma unroll
-        for (int k = KS - kTail; k < KS; ++k) {
-          const uint32_t r2 = u_step_xor(lds, reg ^ word(k), 0u, bu0, bu1);
-          reg = (uint32_t)k < nsl ? r2 : reg;
-        }
+        for (int k = 0; k < KS - kTail - 1; ++k)
+#pragma unroll
+          for (int h = 0; h < WL; ++h) in[h] = u_step_xor(lds, in[h], word(k + 1, h), bu0, bu1);
+#pragma unroll
+        for (int h = 0; h < WL; ++h) reg[h] = u_step_xor(lds, in[h], 0u, bu0, bu1);
+#pragma unroll
+        for (int k = KS - kTail; k < KS; ++k)
+#pragma unroll
+          for (int h = 0; h < WL; ++h) {
+            const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+            reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+          }
       } else {
 #pragma unroll
-        for (int k = 0; k < KS; ++k) {
-          const uint32_t r2 = u_step_xor(lds, reg ^ word(k), 0u, bu0, bu1);
-          reg = (uint32_t)k < nsl ? r2 : reg;
-        }
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int h = 0; h < WL; ++h) {
+            const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+            reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+          }
       }
     }
     Fin fin;
-    fin.reg = reg;
+#pragma unroll
+    for (int h = 0; h < WL; ++h) fin.reg[h] = reg[h];
     fin.junk = jk[s] & ~(uint32_t)(0xFFFFFFFFull >> (8 * (t & 3u)));
     fin.f = it_f[s];
     fin.n = n;
@@ -602,14 +692,41 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     uint32_t crc = 0;
     const uint32_t n = fin.n, t = fin.t;
     if (fin.any) {
-      // the last lane absorbed t junk bytes past the frame end: take their
-      // U-image out (junk is 0 on every other lane, and U(0) = 0)
-      uint32_t r = fin.reg ^ u_step(lds, fin.junk, bu0, bu1);
-      if constexpr (kLine) {  // lane q takes the register of lane q - a (mod 32) of its row
-        const uint32_t src = (row << 5) | ((p - (t >> 2)) & 31u);
-        r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)r);
+      // the lane holding the frame end absorbed t & 3 junk bytes past it: take
+      // their U-image out (junk is 0 on every other lane, and U(0) = 0)
+      uint32_t R;
+      if constexpr (WL == 2) {
+        uint32_t r0 = fin.reg[0], r1 = fin.reg[1];
+        if (wave_any(fin.junk != 0)) {
+          const uint32_t u = u_step(lds, fin.junk, bu0, bu1);
+          const bool odd = ((31u - (t >> 2)) & 1u) != 0;  // virtual lane 31 - a is register (31 - a) & 1
+          r0 ^= odd ? 0u : u;
+          r1 ^= odd ? u : 0u;
+        }
+        // rows 2m, 2m+1 (lanes 32m .. 32m+31): lane c of the pair applies its
+        // own F_c to virtual lane (c - a) mod 32 of each of the two frames
+        const auto ts = __builtin_amdgcn_permlane16_swap(t, t, false, false);  // t of row 2m, of row 2m+1
+        const uint32_t c = lane & 31u, base = lane & 32u;
+        const uint32_t vA = (c - (ts[0] >> 2)) & 31u, vB = (c - (ts[1] >> 2)) & 31u;
+        const int sA = (int)((base | (vA >> 1)) << 2), sB = (int)((base | 16u | (vB >> 1)) << 2);
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sA, (int)r0);
+        const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sA, (int)r1);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sB, (int)r0);
+        const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sB, (int)r1);
+        const uint32_t fA = row_xor<16>(f_step(lds, (vA & 1u) ? a1 : a0, bf));
+        const uint32_t fB = row_xor<16>(f_step(lds, (vB & 1u) ? b1 : b0, bf));
+        // the pair's halves: row 2m gets fA.h0 ^ fA.h1, row 2m+1 fB.h0 ^ fB.h1
+        const auto sw = __builtin_amdgcn_permlane16_swap(fA, fB, false, false);
+        R = t_fix<16>(lds, sw[0] ^ sw[1], t & 3u, p, bt);
+      } else {
+        uint32_t r = fin.reg[0];
+        if (wave_any(fin.junk != 0)) r ^= u_step(lds, fin.junk, bu0, bu1);
+        if constexpr (kLine) {  // lane q takes the register of lane q - a (mod 32) of its row
+          const uint32_t src = (row << 5) | ((p - (t >> 2)) & 31u);
+          r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)r);
+        }
+        R = t_fix<RL>(lds, row_xor<RL>(f_step(lds, r, bf)), t & 3u, p, bt);
       }
-      uint32_t R = t_fix<RL>(lds, row_xor<RL>(f_step(lds, r, bf)), t & 3u, p, bt);
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
       crc = ~R;
@@ -663,19 +780,22 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 
 // ------------------------------------------------------------------ kernel
 // Row width per workgroup from its frames' mean length (RLF = 0): 4-lane rows
-// below kShortMean, 32-lane rows from kLineMean on, 16-lane rows between; or
-// forced (RLF = 4 / 16 / 32, profiling).  Item size, ring depth and chunk:
-// KSW, SW, CHW for 32-lane rows (for 16-lane rows too when forced; auto mode
-// gives them 24, 1, 4), KS4, S4, CH4 for 4-lane rows.
+// below kShortMean, 32-lane rows from kLineMean on, 16-lane rows with MIDW
+// words per lane between; or forced (RLF = 4 / 16 / 32, profiling).  Item
+// size, ring depth and chunk: KSW, SW, CHW for 32-lane rows, KSM, SM, CHM
+// for 16-lane rows, KS4, S4, CH4 for 4-lane rows.
 //
-// Why three widths: 32-lane rows read whole lines with nt loads and reach
-// 6.5-6.65 TB/s on 9000-byte frames, but they finish 2 frames per wave-slot
-// where 16-lane rows finish 4, and at 1500 bytes (one 13-line item per frame)
-// that per-frame work makes them VALU-bound (4.9 TB/s against 5.8 for
-// 16-lane rows).
+// 32-lane rows and 16-lane rows of two words per lane both read whole lines
+// with nt loads (loads alone: 6.4 TB/s at 1500 B against 6.0 for one-word
+// 16-lane rows), and both win at 9000 B (6.70 / 6.74 TB/s against 6.14).  At
+// 1500 B (one 13-line item per frame) their per-frame finish costs more:
+// 32-lane rows finish 2 frames per wave-slot where 16-lane rows finish 4
+// (VALU-bound, 4.9 TB/s), and two-word rows apply F to 32 registers per frame
+// (5.7-5.8 TB/s against 5.9 for one-word rows).  So MIDW = 1 in the product
+// (profiles/r1f_line_rows_variants.txt).
 constexpr uint64_t kLineMean = 4096;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 12, int S4 = 2,
-          int CHW = 4, int CH4 = 16, bool SEG = false>
+          int CHW = 4, int CH4 = 16, bool SEG = false, int MIDW = 1, int KSM = 24, int SM = 1, int CHM = 4>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -701,6 +821,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     rl = nf_ == 0 || nb_ < kShortMean * nf_ ? 4 : nb_ < kLineMean * nf_ ? 16 : 32;
   }
   const bool narrow = rl == 4;
+  const bool line = rl == 32 || (rl == 16 && MIDW == 2);  // whole-line windows: the RL = 32 image
   {
     // compact image (lds_layout.hpp): thread t expands U value t into its 32
     // bank replicas (128 contiguous bytes, eight 16-byte writes started at a
@@ -709,7 +830,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // the chunk counter at 0
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          image_index(rl) * kCompactDwords;
+                          image_index(line ? 32 : rl) * kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
     const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
@@ -747,7 +868,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   // A range (a workgroup's slice of frames) is addressed through one buffer
   // descriptor whose base is 4-byte aligned (128-byte aligned for 32-lane
   // rows, whose windows run between lines): rel(x) = x - off[fb0] + adj.
-  const uint32_t amask = rl == 32 ? 127u : 3u;
+  const uint32_t amask = line ? 127u : 3u;
   struct Range {
     uint64_t f0, f1, o0, o1;
     bool fits;  // byte range within 31-bit buffer offsets
@@ -788,10 +909,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
-    } else if (rl == 16) {
+    } else if (!line) {
       L.p = lane & 15u, L.row = lane >> 4;
       rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
-    } else {
+    } else {  // the RL = 32 image: 32-lane rows
       L.p = lane & 31u, L.row = lane >> 5;
       rows_generic<MODE, 32>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
     }
@@ -804,7 +925,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, RLF == 16 ? KSW : 24, RLF == 16 ? SW : 1, RLF == 16 ? CHW : 4, VAR, SEG>(lds, L, cx);
+      rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW>(lds, L, cx);
     } else if (RLF != 16) {
       L.p = lane & 31u, L.row = lane >> 5;
       rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG>(lds, L, cx);
@@ -836,9 +957,15 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
     // profiling variants (tools/prof/variants.py).  Arguments:
-    // VAR, forced row width (0 = per workgroup), KSW, SW, KS4, S4, CHW, CH4
+    // VAR, forced row width (0 = per workgroup), KSW, SW, KS4, S4, CHW, CH4,
+    // SEG, MIDW, KSM, SM, CHM
+#define LNX_16(W, KS_, S_, CH_) LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16, false, W, KS_, S_, CH_)
     switch (var) {
-      // 10-16: forced 32-lane rows (KSW, SW, CHW vary); 17: forced 16-lane rows
+      case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
+      case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
+      case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
+      case 5: LNX_LAUNCH(CrcMode::kCrc, 5); break;  // clock-window flushes for 4-lane rows too
+      // 10-16: forced 32-lane rows (KSW, SW, CHW vary)
       case 10: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 1, 12, 2, 4, 16); break;  // one 13-line item per 1500 B
       case 11: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 2, 12, 2, 4, 16); break;  // two-slot ring
       case 12: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 14, 1, 12, 2, 4, 16); break;
@@ -846,33 +973,26 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 14: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 13, 1, 12, 2, 8, 16); break;  // 8-frame chunks
       case 15: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 24, 1, 12, 2, 4, 16); break;  // 24-line items
       case 16: LNX_LAUNCH(CrcMode::kCrc, 0, 32, 18, 1, 12, 2, 4, 16); break;
-      case 17: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16); break;
-      case 1: LNX_LAUNCH(CrcMode::kCrc, 1); break;  // loads + bookkeeping only
-      case 2: LNX_LAUNCH(CrcMode::kCrc, 2); break;  // lookups + bookkeeping only
-      case 3: LNX_LAUNCH(CrcMode::kCrc, 3); break;  // bounds window loaded by all 64 lanes
-      case 5: LNX_LAUNCH(CrcMode::kCrc, 5); break;  // clock-window flushes for 4-lane rows too
-      case 20: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16); break;  // forced 16-lane rows
-      case 21: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 12, 3, 16, 1, 4, 16); break;
-      case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;  // forced 4-lane rows
+      // forced 16-lane rows: one word per lane (17, 21), two words per lane (18, 19, 28, 29, 40-42)
+      case 17: LNX_16(1, 24, 1, 4); break;  // round-1 product
+      case 21: LNX_16(1, 12, 3, 4); break;
+      case 18: LNX_16(2, 13, 1, 4); break;  // one 13-line item per 1500 B
+      case 19: LNX_16(2, 13, 2, 4); break;  // two-slot ring
+      case 28: LNX_16(2, 14, 1, 4); break;
+      case 29: LNX_16(2, 24, 1, 4); break;  // 24-line items
+      case 40: LNX_16(2, 13, 1, 8); break;  // 8-frame chunks
+      case 41: LNX_16(2, 12, 2, 4); break;
+      case 42: LNX_16(2, 13, 1, 16); break;
+      // forced 4-lane rows
+      case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 8, 3, 4, 64); break;
       case 24: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 32); break;
       case 25: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 6, 3, 4, 64); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
-      case 29: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 2, 16, 1, 32, 16); break;  // 32-frame chunks
-      case 30: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 8, 3, 16, 64); break;  // round-1 product: two-slot rings
-      case 31: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 8, 16); break;  // two-slot ring, 8-frame chunks
-      case 33: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 4, 16); break;  // two-slot ring, 4-frame chunks
-      case 39: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 12, 2, 16, 1, 4, 16); break;  // 12-step items
-      case 43: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 1, 4, 16); break;  // 12-step short items
-      case 45: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 4, 16); break;  // one-slot 16-step short items
-      case 47: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 8, 32); break;
-      case 48: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 16, 16); break;
-      case 49: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 1, 32, 16); break;
-      case 50: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 16, 16); break;
-      case 51: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 2, 16, 1, 32, 16); break;
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
     }
+#undef LNX_16
   }
 #undef LNX_LAUNCH
   return hipGetLastError();

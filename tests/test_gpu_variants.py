@@ -19,10 +19,11 @@ pytestmark = pytest.mark.gpu
 
 # 10..16: forced 32-lane rows (line-aligned windows, nt loads), (KS, S) = (13, 1), (13, 2),
 #   (14, 1), (13, 1) with 2- and 8-frame chunks, (24, 1), (18, 1);
-# 17/20/21: forced 16-lane rows, (KS, S) = (24, 1), (24, 1), (12, 3); 29: (24, 2) with 32-frame chunks;
-# 22..25: forced 4-lane rows (16, 1), (8, 3), (12, 2), (6, 3);
-# 30/31/33/39/43/45/47: per-workgroup row width with other item / ring / chunk shapes
-FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 20, 21, 22, 23, 24, 25, 29, 30, 31, 33, 39, 43, 45, 47]
+# 17/21: forced one-word 16-lane rows, (KS, S) = (24, 1), (12, 3);
+# 18/19/28/29/40/41/42: forced two-word 16-lane rows (line windows, dwordx2 nt loads),
+#   (13, 1), (13, 2), (14, 1), (24, 1), (13, 1) with 8- and 16-frame chunks, (12, 2);
+# 22..25: forced 4-lane rows (16, 1), (8, 3), (12, 2), (6, 3)
+FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

@@ -11,8 +11,10 @@ OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="bench.py --workload $WL --no-cpu-baseline"
+BT="$B --prewarm-s 0.2"
+B="$B --prewarm-s 0"
 echo "[prof] kernel trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 $B --steps 20 --warmup 3 > $OUT/bench_trace.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace --output-format csv -- python3 $BT --steps 20 --warmup 3 > $OUT/bench_trace.log 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 i=0
 for CNT in "FETCH_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
   i=$((i+1))

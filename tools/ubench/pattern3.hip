@@ -145,31 +145,16 @@ int main(int argc, char** argv) {
 #define RUN(W, RL, D, A, P) RUNR(W, RL, D, A, P, false)
   printf("frames %u x %u B\n", nframes, fb);
   RUN(4, 16, 16, 64, 0);
-  RUNR(4, 32, 16, 128, 2, true);
-  RUNR(4, 32, 12, 128, 2, true);
-  RUNR(4, 32, 24, 128, 2, true);
-  RUNR(4, 32, 16, 128, 18, true);
-  RUNR(4, 32, 16, 128, 0, true);
-  RUN(4, 32, 12, 128, 2);
-  RUN(4, 32, 24, 128, 2);
-  RUN(4, 16, 16, 64, 2);
-  RUN(4, 32, 16, 128, 0);
+  RUN(4, 32, 13, 128, 2);
   RUN(4, 32, 16, 128, 2);
-  RUN(8, 16, 8, 128, 0);
   RUN(8, 16, 8, 128, 2);
-  RUN(16, 16, 4, 256, 0);
-  RUN(16, 16, 4, 256, 2);
-  RUN(16, 16, 6, 256, 2);
-  RUN(16, 16, 8, 256, 2);
-  RUN(16, 16, 6, 128, 2);
-  RUN(16, 16, 6, 64, 2);
-  RUN(16, 16, 6, 16, 2);
-  RUN(16, 32, 4, 512, 2);
-  RUN(16, 32, 4, 128, 2);
-  RUN(16, 64, 4, 1024, 2);
-  RUN(16, 64, 4, 128, 2);
-  RUN(16, 16, 6, 128, 0);
-  RUN(16, 16, 6, 128, 16);
-  RUN(16, 16, 6, 128, 18);
+  RUN(8, 16, 12, 128, 2);
+  RUN(8, 16, 13, 128, 2);
+  RUN(8, 16, 16, 128, 2);
+  RUN(8, 16, 24, 128, 2);
+  RUNR(8, 16, 13, 128, 2, true);
+  RUN(8, 16, 13, 128, 0);
+  RUN(8, 16, 13, 128, 18);
+  RUN(8, 8, 12, 128, 2);
   return 0;
 }
