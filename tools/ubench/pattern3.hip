@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t fold(uint32_t v) { return v; }
 __device__ __forceinline__ uint32_t fold(u32x2 v) { return v[0] ^ v[1]; }
 __device__ __forceinline__ uint32_t fold(u32x4 v) { return v[0] ^ v[1] ^ v[2] ^ v[3]; }
 
-template <int W, int RL, int D, int A, int P, bool RELOAD = false>
+template <int W, int RL, int D, int A, int P, bool RELOAD = false, int P2 = P>
 __global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, uint32_t nbytes, uint32_t nframes,
                                             uint32_t fb, uint32_t fpw, uint32_t* out) {
   __shared__ uint32_t pad[40960];
@@ -88,13 +88,13 @@ __global__ void __launch_bounds__(1024) pat(const uint8_t* __restrict__ base, ui
   };
   typename Vt<W>::T v[D];
 #pragma unroll
-  for (int u = 0; u < D; ++u) v[u] = ldv<W, P>(r, next());
+  for (int u = 0; u < D; ++u) v[u] = (u & 1) ? ldv<W, P2>(r, next()) : ldv<W, P>(r, next());
   uint32_t acc = 0;
   for (;;) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       acc ^= fold(v[u]);
-      v[u] = ldv<W, P>(r, next());
+      v[u] = (u & 1) ? ldv<W, P2>(r, next()) : ldv<W, P>(r, next());
       if constexpr (RELOAD) acc ^= __builtin_amdgcn_raw_buffer_load_b32(r, jo, 0, P);
     }
     if (!__builtin_amdgcn_ballot_w64(f < f1)) break;
@@ -144,17 +144,16 @@ int main(int argc, char** argv) {
   }
 #define RUN(W, RL, D, A, P) RUNR(W, RL, D, A, P, false)
   printf("frames %u x %u B\n", nframes, fb);
+#define RUNA(P, P2) { float ms = tm([&] { pat<4, 16, 16, 128, P, false, P2><<<256, 1024>>>(buf, nbytes, nframes, fb, fpw, out); }); \
+  printf("W= 4 RL=16 D=16 align=128 pol even/odd step %2d/%2d : %.4f ms %.1f GB/s\n", P, P2, ms, nbytes / ms / 1e6); }
   RUN(4, 16, 16, 64, 0);
-  RUN(4, 32, 13, 128, 2);
+  RUNA(0, 0);
+  RUNA(2, 2);
+  RUNA(0, 2);
+  RUNA(2, 0);
+  RUNA(1, 2);
+  RUNA(0, 18);
+  RUNA(16, 2);
   RUN(4, 32, 16, 128, 2);
-  RUN(8, 16, 8, 128, 2);
-  RUN(8, 16, 12, 128, 2);
-  RUN(8, 16, 13, 128, 2);
-  RUN(8, 16, 16, 128, 2);
-  RUN(8, 16, 24, 128, 2);
-  RUNR(8, 16, 13, 128, 2, true);
-  RUN(8, 16, 13, 128, 0);
-  RUN(8, 16, 13, 128, 18);
-  RUN(8, 8, 12, 128, 2);
   return 0;
 }
