@@ -347,8 +347,9 @@ int lnx_device_count(void) {
 const char* lnx_last_error(void) { return g_last_error.c_str(); }
 
 const char* lnx_version(void) {
-  return "lneto_amd 0.3 gfx950: crc32 rows (16-lane rows: 1 slot x 24 steps, 4-frame chunks; 4-lane rows: "
-         "2 slots x 12 steps, held results) + sum16 16-lane rows + ingress verdicts + rx ring";
+  return "lneto_amd 0.4 gfx950: crc32 rows (32-lane whole-line nt rows from 4096 B mean: 24-line items; "
+         "16-lane rows: 1 slot x 24 steps, 4-frame chunks; 4-lane rows: 2 slots x 12 steps, held results) "
+         "+ sum16 16-lane rows + ingress verdicts + rx ring";
 }
 
 }  // extern "C"
