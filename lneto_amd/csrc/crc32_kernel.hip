@@ -87,16 +87,23 @@ __device__ __forceinline__ uint32_t u_step_xor(const char* lds, uint32_t x, uint
   return __builtin_amdgcn_bitop3_b32(t, lds_rd(lds, a3 + 128), y, 0x96);
 }
 
-// F_p(r) through eight lane-private nibble tables: per nibble one v_bfe and
-// one v_lshl_add for the address (the table offset rides in the ds_read
-// immediate), the eight values XOR-ed by three v_bitop3 and a v_xor.
+// F_p(r) through eight lane-private nibble tables (pairs interleaved, see
+// lds_layout.hpp): the even nibbles are the bytes of r & 0x0F0F0F0F, the odd
+// ones those of (r >> 4) & 0x0F0F0F0F, so each address is one v_perm with the
+// lane base bf (the table offset rides in the ds_read immediate); the eight
+// values are XOR-ed by three v_bitop3 and a v_xor: 14 VALU, 8 LDS.
 __device__ __forceinline__ uint32_t f_step(const char* lds, uint32_t r, uint32_t bf) {
+  const uint32_t y = r & 0x0F0F0F0Fu, z = (r >> 4) & 0x0F0F0F0Fu;
   uint32_t v[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = lds_rd(lds, (__builtin_amdgcn_ubfe(r, 4 * i, 4) << 7) + bf + (uint32_t)(i << 11));
-  const uint32_t x = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
-  const uint32_t y = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
-  return __builtin_amdgcn_bitop3_b32(x, y, v[6] ^ v[7], 0x96);
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = lds_rd(lds, __builtin_amdgcn_perm(y, bf, 0x0c020400u + ((uint32_t)k << 8)) + (uint32_t)(k << 12));
+    v[2 * k + 1] =
+        lds_rd(lds, __builtin_amdgcn_perm(z, bf, 0x0c020400u + ((uint32_t)k << 8)) + (uint32_t)((k << 12) + 128));
+  }
+  const uint32_t a = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
+  const uint32_t b = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
+  return __builtin_amdgcn_bitop3_b32(a, b, v[6] ^ v[7], 0x96);
 }
 
 // v ^ (v moved by the DPP control): bound_ctrl lets hipcc fold the move into
@@ -171,7 +178,7 @@ __device__ __forceinline__ uint32_t ld_buf(uint32_t voff, __amdgpu_buffer_rsrc_t
   return r;
 }
 
-#define LNX_O(k) [o##k] "=v"(o[k])
+#define LNX_O(k) [o##k] "=&v"(o[k])
 #define LNX_I(k) [i##k] "i"(IMM0 + (k) * D)
 // N (1..6) loads from one VGPR offset at immediates IMM0, IMM0 + D, ...
 // NT: non-temporal policy.  Only rows that read whole 128-byte lines per
@@ -248,7 +255,7 @@ __device__ __forceinline__ void ld_item(uint32_t* w, uint32_t v, __amdgpu_buffer
 
 // The same with dwordx2 loads (two words per lane; always non-temporal).
 #define LNX_L(k) "buffer_load_dwordx2 %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "] nt\n\t"
-#define LNX_O(k) [o##k] "=v"(o[k])
+#define LNX_O(k) [o##k] "=&v"(o[k])
 #define LNX_I(k) [i##k] "i"(IMM0 + (k) * D)
 template <int IMM0, int N, int D>
 __device__ __forceinline__ void ld_run2(uint64_t* o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
@@ -778,6 +785,249 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------ lean line rows
+// Two-word 16-lane rows (buffer_load_dwordx2 nt: each row instruction reads one
+// whole 128-byte line) with the per-slot bookkeeping cut to what frames of up
+// to KS lines need (DESIGN.md §3.1 "lean line rows").  rows_body spends
+// ~130-160 VALU per wave-slot on item cursors, ballot ranks, bounds windows and
+// multi-chunk frame lookups (PMC: 82 VALU per 1500-B frame for one-word rows,
+// 117 for two-word rows); here:
+//  * a chunk is exactly one slot: CH = 4 frames, one per row, claimed from the
+//    LDS counter two slots ahead; its 5 offsets arrive in lanes 0..4 one slot
+//    ahead and reach the rows with two ds_bpermute;
+//  * every row folds its whole frame in the slot: window = the lines holding
+//    the frame (J = 1..KS of them), loads from the window start, the last two
+//    steps predicated (frames of J = KS - 1 or KS lines, e.g. 1500 B at any
+//    alignment with KS = 13); any other J predicates every step, and frames of
+//    more than KS lines take further items inside the slot (correct, slower);
+//  * no register rotation: virtual lane v's register ends 4((v + a) mod 32) + b
+//    bytes past the frame end (t = 4a + b window bytes follow it), so it takes
+//    F_{(v+a) mod 32} straight from that column of the RL = 32 image.  A lane
+//    applies F to its two registers in two instructions; which register goes
+//    first is chosen per row so that the 32 lanes of two rows always read 32
+//    distinct banks (rows 2m and 2m+1 differ in column parity).  One row XOR
+//    of the two F results, then Z_{-b}.
+template <CrcMode MODE, int KS, int VAR>
+__device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
+  constexpr uint32_t CH = 4;  // frames per chunk = rows per wave
+  static_assert(KS >= 4 && (KS - 1) * 128 <= 4095, "item shape");
+  const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bt = L.bt;
+  const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
+  const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
+
+  // a claim's result stays in lane 0's VGPR until the next slot reads it
+  // (readfirstlane), so the wave never waits on the LDS atomic's latency
+  auto claim = [&]() -> uint32_t {
+    uint32_t b = 0;
+    if (lane == 0) b = __hip_atomic_fetch_add(cx.ctr, CH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return b;
+  };
+  auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  // lane i < 5: low dword of off[b + i] (the range's offsets array has nfb + 1 entries)
+  auto ld_bounds = [&](uint32_t b) -> uint32_t {
+    return ld_buf<0>(b < nfb && lane <= CH ? (b + lane) * 8u : kOOB, off_rsrc);
+  };
+
+  // row-uniform parameters of the frame in progress
+  struct Rowp {
+    uint32_t f, n, t, J, ws;
+  };
+  auto setup = [&](uint32_t b, uint32_t bd) -> Rowp {
+    Rowp r;
+    const uint32_t s = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(row << 2), (int)bd);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((row + 1) << 2), (int)bd);
+    const uint32_t f = b + row;
+    const uint32_t len = e - s;
+    r.f = f < nfb ? f : kNoFrame;
+    r.n = f < nfb && (int32_t)len > 0 ? len : 0u;  // end below start: empty frame
+    const uint32_t rs = s - o0_lo + adj, re = e - o0_lo + adj;
+    const uint32_t wend = (re + 127u) & ~127u;
+    r.ws = rs & ~127u;
+    r.t = wend - re;
+    r.J = r.n ? (wend - r.ws) >> 7 : 0u;
+    return r;
+  };
+
+  uint64_t w[KS];
+  uint32_t jk = 0;
+  auto issue = [&](const Rowp& r) {
+    const uint32_t voff = r.J ? r.ws + p * 8u : kOOB;
+    if constexpr (VAR == 2) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) w[k] = (uint64_t)(voff * 0x9E3779B1u + k) * 0x100000001ull;
+    } else {
+      ld_item<0, KS, 128, true>(w, voff, data_rsrc);
+    }
+    // the word holding the frame end, when junk bytes follow it there: virtual lane 31 - a
+    const uint32_t jl = 31u - (r.t >> 2);
+    const bool jn = r.J != 0 && p == (jl >> 1) && (r.t & 3u) != 0;
+    jk = ld_buf<0>(jn ? r.ws + ((r.J - 1u) << 7) + (jl << 2) : kOOB, data_rsrc);
+  };
+
+  struct Fin {
+    uint32_t r0, r1, junk, f, n, t;
+  };
+  auto fold = [&](const Rowp& r) -> Fin {
+    const uint32_t n = r.n, t = r.t, J = r.J, a = t >> 2;
+    const uint32_t lead = (r.J ? (J << 7) - n - t : 0u);
+    const uint32_t m4 = n < 4 ? n : 4u;
+    // step 0: the lane's 8 bytes keep [lead - 8p, 8) and take the init 0xFF
+    // over [lead - 8p, lead - 8p + m4); bytes [d, 8) of a qword are
+    // (~0 << 4d) << 4d for d in 0..8 (two shifts: a 64-bit shift by 64 is 0)
+    auto keep8 = [](int32_t d) -> uint64_t {
+      const uint32_t q = 4u * (uint32_t)(d < 0 ? 0 : (d > 8 ? 8 : d));
+      return (~0ull << q) << q;
+    };
+    const int32_t d0 = (int32_t)lead - (int32_t)(p << 3);
+    const uint64_t keep = keep8(d0), initm = keep & ~keep8(d0 + (int32_t)m4);
+    const uint64_t w0 = (w[0] & keep) ^ initm;
+    uint32_t nsl[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) nsl[h] = J ? J - (2u * p + h >= 32u - a ? 1u : 0u) : 0u;
+    const int32_t x1 = (int32_t)(lead + m4) - 128;  // init bytes spilling into step 1
+    const uint32_t m1 = x1 > 0 && p == 0 ? (uint32_t)((1ull << (8 * x1)) - 1) : 0u;
+    auto word = [&](int k, int h) -> uint32_t {
+      uint32_t x = (uint32_t)((k == 0 ? w0 : w[k]) >> (32 * h));
+      if (k == 1 && h == 0) x ^= m1;
+      return x;
+    };
+    uint32_t reg[2] = {0u, 0u};
+    if constexpr (VAR == 1) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) reg[h] ^= word(k, h);
+    } else {
+      // fast: every row's frame spans KS - 1 or KS lines (or none)
+      const bool fast = !wave_any(J != 0 && J + 1u < (uint32_t)KS) && !wave_any(J > (uint32_t)KS);
+      if (fast) {
+        uint32_t in[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) in[h] = word(0, h);
+#pragma unroll
+        for (int k = 0; k < KS - 3; ++k)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) in[h] = u_step_xor(lds, in[h], word(k + 1, h), bu0, bu1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) reg[h] = u_step_xor(lds, in[h], 0u, bu0, bu1);
+#pragma unroll
+        for (int k = KS - 2; k < KS; ++k)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+            reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+          }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+            reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+          }
+        // frames of more than KS lines: further items, loaded and folded in turn
+        for (uint32_t j0 = KS; wave_any(j0 < J); j0 += KS) {
+          // a separate array: reloading w here would give the ring registers
+          // two definitions and hipcc copies between them at the loop head,
+          // before the ring's wait
+          uint64_t wx[KS];
+          const uint32_t voff = j0 < J ? r.ws + (j0 << 7) + p * 8u : kOOB;
+          ld_item<0, KS, 128, true>(wx, voff, data_rsrc);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(wx[k]));
+#pragma unroll
+          for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t r2 = u_step_xor(lds, reg[h] ^ (uint32_t)(wx[k] >> (32 * h)), 0u, bu0, bu1);
+              reg[h] = j0 + (uint32_t)k < nsl[h] ? r2 : reg[h];
+            }
+        }
+      }
+    }
+    Fin fin;
+    fin.r0 = reg[0];
+    fin.r1 = reg[1];
+    fin.junk = jk & ~(uint32_t)(0xFFFFFFFFull >> (8 * (t & 3u)));
+    fin.f = r.f;
+    fin.n = n;
+    fin.t = t;
+    return fin;
+  };
+
+  // results held in registers, flushed in clock windows (as rows_body)
+  constexpr int kWinLog = 12;
+  uint32_t hf = 0, hv = 0, pc = 0;
+  uint32_t win = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
+  auto finish = [&](const Fin& fin) {
+    const uint32_t n = fin.n, t = fin.t, a = t >> 2;
+    const bool live = fin.f != kNoFrame;
+    uint32_t r0 = fin.r0, r1 = fin.r1;
+    if (wave_any(fin.junk != 0)) {
+      const uint32_t u = u_step(lds, fin.junk, bu0, bu1);
+      const bool odd = ((31u - a) & 1u) != 0;  // virtual lane 31 - a is register (31 - a) & 1
+      r0 ^= odd ? 0u : u;
+      r1 ^= odd ? u : 0u;
+    }
+    // register h of lane p (virtual lane 2p + h) takes F_q, q = (2p + h + a) mod 32;
+    // the odd row of each pair goes first with the register whose column
+    // parity differs from the even row's
+    const auto as = __builtin_amdgcn_permlane16_swap(a, a, false, false);  // a of row 2m, of row 2m+1
+    const uint32_t hs = (row & 1u) ? (((as[0] ^ as[1]) & 1u) ^ 1u) : 0u;
+    const uint32_t x1 = hs ? r1 : r0, x2 = hs ? r0 : r1;
+    const uint32_t q1 = (2u * p + hs + a) & 31u, q2 = (2u * p + (hs ^ 1u) + a) & 31u;
+    const uint32_t F = f_step(lds, x1, kFBase | (q1 << 2)) ^ f_step(lds, x2, kFBase | (q2 << 2));
+    uint32_t R = t_fix<16>(lds, row_xor<16>(F), t & 3u, p, bt);
+    R = n != 0 ? R : 0u;
+    if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    const uint32_t crc = ~R;
+    if (live && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
+    pc += live ? 1u : 0u;
+    bool fl = wave_any(pc == 16u);
+    const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
+    fl = fl || (now != win && wave_any(pc != 0));
+    win = now;
+    if (fl) {
+      store_result<MODE>(out_rsrc, p < pc, hf, hv);
+      pc = 0;
+    }
+  };
+
+  const uint32_t c0 = uni(claim());
+  uint32_t bd = ld_bounds(c0);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(bd));
+  if (c0 >= nfb) return;
+  uint32_t c1 = uni(claim());
+  Rowp cur = setup(c0, bd);
+  issue(cur);
+  bd = ld_bounds(c1);
+  uint32_t c2v = claim();
+#define LNX_FENCE __builtin_amdgcn_sched_barrier(0)
+  for (;;) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(w[k]));
+    asm volatile("" : "+v"(jk), "+v"(bd));
+    const Fin fin = fold(cur);
+    if (c1 >= nfb) {
+      finish(fin);
+      break;
+    }
+    LNX_FENCE;
+    cur = setup(c1, bd);
+    issue(cur);
+    c1 = uni(c2v);
+    bd = ld_bounds(c1);
+    c2v = claim();
+    LNX_FENCE;
+    finish(fin);
+  }
+#undef LNX_FENCE
+  if (wave_any(pc != 0)) store_result<MODE>(out_rsrc, p < pc, hf, hv);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------------------------ kernel
 // Row width per workgroup from its frames' mean length (RLF = 0): 4-lane rows
 // below kShortMean, 32-lane rows from kLineMean on, 16-lane rows with MIDW
@@ -794,8 +1044,12 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // (5.7-5.8 TB/s against 5.9 for one-word rows).  So MIDW = 1 in the product
 // (profiles/r1f_line_rows_variants.txt).
 constexpr uint64_t kLineMean = 4096;
+// Lean line rows (lines_body) from kShortMean up to this mean frame length
+// (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
+constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 12, int S4 = 2,
-          int CHW = 4, int CH4 = 16, bool SEG = false, int MIDW = 1, int KSM = 24, int SM = 1, int CHM = 4>
+          int CHW = 4, int CH4 = 16, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
+          int KSL = 13>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -816,12 +1070,17 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   };
   const uint64_t ob0 = lo_of(fb0, fb1), ob1 = hi_of(fb0, fb1);
   int rl = RLF;
+  // MIDW (16-lane rows): 1 = one word per lane, 2 = two words, 3 = lean line
+  // rows, 4 = lean line rows below kLeanMean, one word per lane above
+  bool lean = MIDW == 3 && !SEG;
   if constexpr (RLF == 0) {
     const uint64_t nf_ = fb1 - fb0, nb_ = ob1 > ob0 ? ob1 - ob0 : 0;
     rl = nf_ == 0 || nb_ < kShortMean * nf_ ? 4 : nb_ < kLineMean * nf_ ? 16 : 32;
+    if (MIDW == 4 && !SEG) lean = rl == 16 && nb_ < kLeanMean * nf_;
   }
   const bool narrow = rl == 4;
-  const bool line = rl == 32 || (rl == 16 && MIDW == 2);  // whole-line windows: the RL = 32 image
+  // whole-line windows: the RL = 32 image
+  const bool line = rl == 32 || (rl == 16 && (MIDW == 2 || lean));
   {
     // compact image (lds_layout.hpp): thread t expands U value t into its 32
     // bank replicas (128 contiguous bytes, eight 16-byte writes started at a
@@ -923,9 +1182,12 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
+    } else if (rl == 16 && lean) {
+      L.p = lane & 15u, L.row = lane >> 4;
+      if constexpr (!SEG) lines_body<MODE, KSL, VAR>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW>(lds, L, cx);
+      rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1>(lds, L, cx);
     } else if (RLF != 16) {
       L.p = lane & 31u, L.row = lane >> 5;
       rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG>(lds, L, cx);
@@ -983,6 +1245,17 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 40: LNX_16(2, 13, 1, 8); break;  // 8-frame chunks
       case 41: LNX_16(2, 12, 2, 4); break;
       case 42: LNX_16(2, 13, 1, 16); break;
+      // forced lean line rows (lines_body): KSL 13 / 14 / 12, loads only, math only
+#define LNX_LEAN(V, KSL_) LNX_LAUNCH(CrcMode::kCrc, V, 16, 24, 1, 12, 2, 4, 16, false, 3, 24, 1, 4, KSL_)
+      case 50: LNX_LEAN(0, 13); break;
+      case 51: LNX_LEAN(0, 14); break;
+      case 52: LNX_LEAN(0, 12); break;
+      case 53: LNX_LEAN(1, 13); break;
+      case 54: LNX_LEAN(2, 13); break;
+      case 55: LNX_LEAN(0, 24); break;
+      // product dispatch with one-word 16-lane rows instead of lean rows (the r1f product)
+      case 56: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 1); break;
+#undef LNX_LEAN
       // forced 4-lane rows
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 8, 3, 4, 64); break;

@@ -21,10 +21,15 @@
 // base; m&1 is folded into the ds_read immediate offset (+128).
 //
 // F region [128 KiB, 144 KiB): per-lane final alignment F_p = Z_{-4p} (lane p's
-// register ends 4p bytes past the window end) as eight 16-entry nibble tables:
-//     byte address = 128K | i<<11 | v<<7 | c<<2          (nibble i, value v)
+// register ends 4p bytes past the window end) as eight 16-entry nibble tables,
+// interleaved in pairs like the U tables (nibbles 2k and 2k+1 share 256-byte
+// rows):
+//     byte address = 128K | (i>>1)<<12 | v<<8 | (i&1)<<7 | c<<2   (nibble i, value v)
 // F_p(r) = XOR_i F_p,i[(r >> 4i) & 15]; column c holds the tables of
-// p = c % RL, which serves lanes c and c+32 alike.
+// p = c % RL, which serves lanes c and c+32 alike.  With y = r & 0x0F0F0F0F and
+// z = (r >> 4) & 0x0F0F0F0F, nibble 2k is byte k of y and nibble 2k+1 byte k
+// of z, so every address is one v_perm of y or z with the lane's base (byte 1
+// = the nibble, byte 2 = 0x02 from 128K) plus an immediate (k<<12 | (i&1)<<7).
 //
 // T region [144 KiB, 156 KiB): the window ends at the frame end rounded up to
 // 4 bytes, t = 0..3 bytes past it, so the row's register needs Z_{-t} too.  The
@@ -52,7 +57,7 @@ constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
   return ((m >> 1) << 16) | (e << 8) | ((m & 1) << 7) | (c << 2);
 }
 constexpr uint32_t f_addr(uint32_t c, uint32_t nib, uint32_t v) {
-  return kFBase | (nib << 11) | (v << 7) | (c << 2);
+  return kFBase | ((nib >> 1) << 12) | (v << 8) | ((nib & 1) << 7) | (c << 2);
 }
 constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // t = 1..3
   return kTBase + ((48u * h + 16u * (t - 1) + v) << 7) + (c << 2);

@@ -95,6 +95,11 @@ WORKLOADS = {
     "jumbo9000": dict(kind="fixed", length=9000, n=1 << 20),
     "zipf64_1500": dict(kind="zipf", n=1 << 24),
     "mtu1500_x8": dict(kind="fixed", length=1500, n=1 << 27),
+    # dispatch-tuning workloads (not bench configs): row-width thresholds
+    "fixed1024": dict(kind="fixed", length=1024, n=1 << 20),
+    "fixed2048": dict(kind="fixed", length=2048, n=1 << 20),
+    "fixed3072": dict(kind="fixed", length=3072, n=1 << 19),
+    "uni640_1536": dict(kind="uniform", lo=640, hi=1536, n=1 << 21),
 }
 
 
@@ -103,4 +108,7 @@ def workload_offsets(name: str, n: int | None = None) -> np.ndarray:
     n = w["n"] if n is None else n
     if w["kind"] == "fixed":
         return fixed_offsets(n, w["length"])
+    if w["kind"] == "uniform":
+        rng = np.random.default_rng(ZIPF_SEED)
+        return offsets_from_lengths(rng.integers(w["lo"], w["hi"] + 1, size=n))
     return offsets_from_lengths(zipf_lengths(n))

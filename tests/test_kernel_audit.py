@@ -21,7 +21,8 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path):
-    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-c", "--save-temps",
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+                    "-c", "--save-temps",
                     "-o", str(tmp_path / "k.o"), SRC], cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
     text = open(tmp_path / asm).read()

@@ -59,6 +59,12 @@ def main():
             continue
         ev, d = vmem_dest(t)
         if ev:
+            # a later load of the same asm run whose offset VGPR is an earlier
+            # load's destination (outputs not early-clobber): if the earlier
+            # load returns before this one issues, the offset is garbage
+            srcs = regs(t.partition(" ")[2].partition(",")[2]) if d else regs(t.partition(" ")[2])
+            if srcs & pending:
+                bad.append((i, t, "reads a register an outstanding load will overwrite"))
             pending |= d
             seq.append(frozenset(d))
             continue
