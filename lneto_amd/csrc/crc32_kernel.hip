@@ -856,7 +856,11 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
 #pragma unroll
       for (int k = 0; k < KS; ++k) w[k] = (uint64_t)(voff * 0x9E3779B1u + k) * 0x100000001ull;
     } else {
-      ld_item<0, KS, 128, true>(w, voff, data_rsrc);
+      // the last step from its own offset: out of range unless the frame has
+      // KS lines (a 1500-B frame spans 12 lines at 29 % of start alignments;
+      // the 13th line belongs to the next frame and would be fetched twice)
+      ld_item<0, KS - 1, 128, true>(w, voff, data_rsrc);
+      ld_run2<(KS - 1) * 128, 1, 128>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
     }
     // the word holding the frame end, when junk bytes follow it there: virtual lane 31 - a
     const uint32_t jl = 31u - (r.t >> 2);
