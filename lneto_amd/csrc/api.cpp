@@ -30,7 +30,7 @@ hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* le
                              hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
-                                 hipStream_t stream);
+                                 hipStream_t stream, int var = 0);
 
 // The 160 KiB LDS image of row width rl (lds_layout.hpp), built once on the host.
 std::vector<uint32_t> build_lds_image(uint32_t rl) {
@@ -319,6 +319,21 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                       static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
+  return LNX_OK;
+}
+
+// Profiling hook: sum16 kernel variants (0 = line rows, the product; 1 = the
+// r1c half-line rows).
+int lnx__sum16_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
+                       const uint32_t* d_seed, uint64_t n, uint16_t* d_out, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_len || !d_out) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_sum16_segments(d_bytes, d_off, d_len, d_seed, n, d_out, c->num_cus,
+                                       static_cast<hipStream_t>(stream), var);
+  if (e != hipSuccess) return hip_fail(e, "sum16 variant launch");
   return LNX_OK;
 }
 

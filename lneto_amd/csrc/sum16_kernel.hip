@@ -87,16 +87,85 @@ sum16_segments_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
   }
 }
 
+// Line rows (round 1, r1g): the same row-per-segment split, but lane p loads
+// 8 bytes (global_load_dwordx2 nt) at 8p + 128k of the segment's 128-byte
+// aligned span, so every row instruction reads one whole line — the pattern
+// whose non-temporal streaming rate is 6.4-6.5 TB/s against 6.0 for the
+// 64-byte half lines above (DESIGN.md §3.1 "whole-line rows").  kLineUnroll
+// lines per row in flight.
+constexpr int kLineUnroll = 8;
+
+__device__ __forceinline__ uint64_t keep8(int32_t d) {  // bytes [d, 8) of a qword, d clamped to 0..8
+  const uint32_t q = 4u * (uint32_t)(d < 0 ? 0 : (d > 8 ? 8 : d));
+  return (~0ull << q) << q;
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(kSumBlock)
+sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                   const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed, uint64_t nseg,
+                   uint16_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
+  const uint64_t nwaves = (uint64_t)gridDim.x * kSumWaves;
+  for (uint64_t q = (uint64_t)blockIdx.x * kSumWaves + (threadIdx.x >> 6); q * 4 < nseg; q += nwaves) {
+    const uint64_t i = q * 4 + row;
+    const bool live = i < nseg;
+    const uint64_t s = live ? off[i] : 0;
+    const uint32_t L = live ? len[i] : 0u;
+    const uint32_t sd = live && seed ? seed[i] : 0u;
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(bytes) + s) & 127u);
+    const uint64_t* base = reinterpret_cast<const uint64_t*>(bytes + s - mis) + p;
+    const uint32_t nl = L ? (mis + L + 127u) >> 7 : 0u;  // lines touching the segment
+    const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;
+    const uint32_t wO = (mis & 1u) ? 0x00010001u : 0x01000100u;
+    uint32_t E = 0, O = 0;
+    // One wave-uniform loop over the largest line count of the four rows.  A
+    // loop bounded by each row's own count (divergent exits, a scalar line
+    // counter, exec-masked loads) came out wrong for ~1 % of the segments of
+    // workgroups 256 and up, differently each launch, on MI355X
+    // (tools/debug/dbg_sum16.py); this form never did.
+    uint32_t nlw = max(nl, (uint32_t)__shfl_xor((int)nl, 16));
+    nlw = max(nlw, (uint32_t)__shfl_xor((int)nlw, 32));
+    nlw = (uint32_t)__builtin_amdgcn_readfirstlane((int)nlw);
+    for (uint32_t k0 = 0; k0 < nlw; k0 += kLineUnroll) {
+      uint64_t x[kLineUnroll];
+#pragma unroll
+      for (int u = 0; u < kLineUnroll; ++u)
+        x[u] = k0 + u < nl ? (NT ? __builtin_nontemporal_load(base + 16u * (k0 + u)) : base[16u * (k0 + u)]) : 0ull;
+#pragma unroll
+      for (int u = 0; u < kLineUnroll; ++u) {
+        const int32_t o0 = (int32_t)(128u * (k0 + u) + 8u * p) - (int32_t)mis;  // segment offset of byte 0
+        const uint64_t y = x[u] & keep8(-o0) & ~keep8((int32_t)L - o0);
+        E = __builtin_amdgcn_udot4((uint32_t)y, wE, E, false);
+        O = __builtin_amdgcn_udot4((uint32_t)y, wO, O, false);
+        E = __builtin_amdgcn_udot4((uint32_t)(y >> 32), wE, E, false);
+        O = __builtin_amdgcn_udot4((uint32_t)(y >> 32), wO, O, false);
+      }
+    }
+    E = row_add16(E);
+    O = row_add16(O);
+    if (live && p == 0) out[i] = fold_sum16(sd + 256u * E + O);
+  }
+}
+
+// var 0: line rows (product); var 1: the half-line rows of sum16_segments_kernel; var 2: line rows, default cache policy
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                   const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, int var) {
   if (n == 0) return hipSuccess;
   const uint64_t seg_per_block = kSumWaves * 4;
   uint64_t grid = (n + seg_per_block - 1) / seg_per_block;
   const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
-  hipLaunchKernelGGL(sum16_segments_kernel, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
-                     off, len, seed, n, out);
+  if (var == 1)
+    hipLaunchKernelGGL(sum16_segments_kernel, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
+                       off, len, seed, n, out);
+  else if (var == 2)
+    hipLaunchKernelGGL(sum16_lines_kernel<false>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,
+                       len, seed, n, out);
+  else
+    hipLaunchKernelGGL(sum16_lines_kernel<true>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,
+                       len, seed, n, out);
   return hipGetLastError();
 }
 

@@ -274,3 +274,33 @@ def test_host_convenience(cuda):
     data = synth.bytes_np(int(off[-1]), seed=9)
     got = L.crc32_batch_host(data, off, device=0)
     assert np.array_equal(got, O.crc32_frames(data, off))
+
+
+def test_sum16_kernel_variants_agree(cuda):
+    """The sum16 kernels (line rows nt = product, half-line rows = r1c, line rows
+    with the default cache policy) on random segments at every start alignment
+    mod 128, lengths 0..2000, 8192 segments (more workgroups than CUs), three
+    launches each."""
+    import ctypes
+    import torch
+    L.lib.lnx__sum16_variant.restype = ctypes.c_int
+    L.lib.lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + \
+        [ctypes.c_void_p] * 2
+    rng = np.random.default_rng(23)
+    n = 8192
+    blob = synth.bytes_np(1 << 21, seed=78)
+    lens = rng.integers(0, 2001, size=n).astype(np.uint32)
+    starts = (rng.integers(0, (len(blob) - 4096) // 128, size=n) * 128 + np.arange(n) % 128).astype(np.uint64)
+    seeds = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    want = O.sum16_segments(blob, starts, lens, seeds)
+    d = torch.from_numpy(blob).to(cuda)
+    o = torch.from_numpy(starts.astype(np.int64)).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int32)).to(cuda)
+    sd = torch.from_numpy(seeds.view(np.int32)).to(cuda)
+    for var in (0, 1, 2, 0, 1, 2, 0, 1, 2):
+        out = torch.empty(n, dtype=torch.int16, device=cuda)
+        assert L.lib.lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n,
+                                        out.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        bad = np.nonzero(out.cpu().numpy().view(np.uint16) != want)[0]
+        assert bad.size == 0, f"sum16 variant {var}: {bad.size} wrong, first {bad[:8]}"

@@ -1,0 +1,36 @@
+"""Time the sum16 kernel variants (0 = line rows nt, 1 = r1c half-line rows, 2 = line rows default policy) on
+1 M x 1500-B segments, round-robin medians.  usage: sum16_variants.py [REPS]"""
+import ctypes, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import numpy as np, torch
+import lneto_amd as L
+from lneto_amd import synth
+L.lib.lnx__sum16_variant.restype = ctypes.c_int
+L.lib.lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 2
+dev = torch.device("cuda:0")
+off = synth.workload_offsets("mtu1500")
+n = len(off) - 1
+d = synth.bytes_torch(int(off[-1]), dev)
+o = torch.from_numpy(off[:-1].astype(np.int64)).to(dev)
+ln = torch.from_numpy(np.diff(off).astype(np.int32)).to(dev)
+out = torch.empty(n, dtype=torch.int16, device=dev)
+s = torch.cuda.current_stream()
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+launch = lambda v: L.lib.lnx__sum16_variant(v, d.data_ptr(), o.data_ptr(), ln.data_ptr(), None, n, out.data_ptr(), s.cuda_stream)
+t0 = time.perf_counter()
+while time.perf_counter() - t0 < 0.5:
+    launch(0)
+torch.cuda.synchronize()
+res = {0: [], 1: [], 2: []}
+for r in range(reps):
+    for v in (0, 1, 2):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record(s)
+        for _ in range(20):
+            launch(v)
+        e[1].record(s)
+        torch.cuda.synchronize()
+        res[v].append(e[0].elapsed_time(e[1]) / 20)
+for v in (0, 1, 2):
+    ms = float(np.median(res[v]))
+    print(f"sum16 variant {v}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s  [{' '.join(f'{x:.4f}' for x in res[v])}]")
