@@ -848,18 +848,42 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     return r;
   };
 
+  // wave-uniform min (over rows with lines) and max of a row-uniform J
+  auto wave_min_max = [&](uint32_t J, uint32_t& jmin, uint32_t& jmax) {
+    jmin = ~0u, jmax = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)J, 16 * r);
+      jmax = x > jmax ? x : jmax;
+      jmin = x != 0 && x < jmin ? x : jmin;
+    }
+  };
+
   uint64_t w[KS];
   uint32_t jk = 0;
+  // runs of up to six step loads; a run no row of the wave reaches loads from
+  // an out-of-range offset (no memory traffic).  Always issued: an asm load
+  // under a branch makes hipcc merge its output with the old value by copies
+  // placed before the ring's wait (tools/prof/audit_ring.py caught that).
+  auto ld_runs = [&]<int K0>(auto self, std::integral_constant<int, K0>, uint32_t voff, uint32_t jmax) {
+    if constexpr (K0 < KS - 1) {
+      constexpr int N = KS - 1 - K0 < 6 ? KS - 1 - K0 : 6;
+      ld_run2<K0 * 128, N, 128>(w + K0, (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
+      self(self, std::integral_constant<int, K0 + N>{}, voff, jmax);
+    }
+  };
   auto issue = [&](const Rowp& r) {
     const uint32_t voff = r.J ? r.ws + p * 8u : kOOB;
     if constexpr (VAR == 2) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) w[k] = (uint64_t)(voff * 0x9E3779B1u + k) * 0x100000001ull;
     } else {
+      uint32_t jmin, jmax;
+      wave_min_max(r.J, jmin, jmax);
+      ld_runs(ld_runs, std::integral_constant<int, 0>{}, voff, jmax);
       // the last step from its own offset: out of range unless the frame has
       // KS lines (a 1500-B frame spans 12 lines at 29 % of start alignments;
       // the 13th line belongs to the next frame and would be fetched twice)
-      ld_item<0, KS - 1, 128, true>(w, voff, data_rsrc);
       ld_run2<(KS - 1) * 128, 1, 128>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
     }
     // the word holding the frame end, when junk bytes follow it there: virtual lane 31 - a
@@ -922,26 +946,40 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
             reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
           }
       } else {
+        // any J: step k is skipped when no row has k lines, unpredicated while
+        // every row with lines has more than k + 1, predicated otherwise
+        // (wave-uniform branches; the junk lanes skip their row's last step)
+        uint32_t jmin, jmax;
+        wave_min_max(J, jmin, jmax);
 #pragma unroll
-        for (int k = 0; k < KS; ++k)
+        for (int k = 0; k < KS; ++k) {
+          if ((uint32_t)k >= jmax) continue;  // (no break: the loop must stay unrolled)
+          if ((uint32_t)k + 1u < jmin) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
-            reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+            for (int h = 0; h < 2; ++h) reg[h] = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+          } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+              reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
+            }
           }
+        }
         // frames of more than KS lines: further items, loaded and folded in turn
-        for (uint32_t j0 = KS; wave_any(j0 < J); j0 += KS) {
+        // (six lines at a time: rare, latency-bound, kept small in registers)
+        constexpr int KX = 6;
+        for (uint32_t j0 = KS; wave_any(j0 < J); j0 += KX) {
           // a separate array: reloading w here would give the ring registers
           // two definitions and hipcc copies between them at the loop head,
           // before the ring's wait
-          uint64_t wx[KS];
+          uint64_t wx[KX];
           const uint32_t voff = j0 < J ? r.ws + (j0 << 7) + p * 8u : kOOB;
-          ld_item<0, KS, 128, true>(wx, voff, data_rsrc);
+          ld_item<0, KX, 128, true>(wx, voff, data_rsrc);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-          for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(wx[k]));
+          for (int k = 0; k < KX; ++k) asm volatile("" : "+v"(wx[k]));
 #pragma unroll
-          for (int k = 0; k < KS; ++k)
+          for (int k = 0; k < KX; ++k)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               const uint32_t r2 = u_step_xor(lds, reg[h] ^ (uint32_t)(wx[k] >> (32 * h)), 0u, bu0, bu1);
@@ -1076,6 +1114,8 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   int rl = RLF;
   // MIDW (16-lane rows): 1 = one word per lane, 2 = two words, 3 = lean line
   // rows, 4 = lean line rows below kLeanMean, one word per lane above
+  // (24-line lean items for 1600-3000 B were tried: w[24] pushed the kernel
+  // past its VGPR budget into scratch)
   bool lean = MIDW == 3 && !SEG;
   if constexpr (RLF == 0) {
     const uint64_t nf_ = fb1 - fb0, nb_ = ob1 > ob0 ? ob1 - ob0 : 0;
@@ -1256,7 +1296,6 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 52: LNX_LEAN(0, 12); break;
       case 53: LNX_LEAN(1, 13); break;
       case 54: LNX_LEAN(2, 13); break;
-      case 55: LNX_LEAN(0, 24); break;
       // product dispatch with one-word 16-lane rows instead of lean rows (the r1f product)
       case 56: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 1); break;
 #undef LNX_LEAN
