@@ -5,8 +5,9 @@
 // removal, F_p, row XOR, Z_{-t} fix) against a plain table CRC-32 for every
 // length 0..N at every start alignment and in every row of the wave, for all
 // three row widths (32-lane rows: line-aligned window, junk lanes skipping the
-// last step, register rotation before F).  No GPU: this pins the algebra and
-// the table contents on the CPU.
+// last step, register rotation before F; lean line rows: two words per lane,
+// F columns chosen per virtual lane instead of a rotation).  No GPU: this pins
+// the algebra and the table contents on the CPU.
 // Built and run by tests/test_abi.py.
 #include <cstdint>
 #include <cstdio>
@@ -97,6 +98,55 @@ struct Emu {
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
     return ~R;
   }
+  // Lean line rows (crc32_kernel.hip lines_body): 16 lanes, lane p loads the
+  // 8 bytes at 8p + 128j (virtual lanes v = 2p, 2p + 1), window = the lines
+  // holding the frame, junk lanes v >= 32 - a skip the last step, virtual lane
+  // 31 - a takes its b junk bytes' U-image out, and with no rotation virtual
+  // lane v's register takes F_q, q = (v + a) mod 32, from column q of the
+  // RL = 32 image; then Z_{-b} as t_fix<16> shares it over the row's lanes.
+  uint32_t crc32lean(const std::vector<uint8_t>& buf, uint32_t rs, uint32_t re, uint32_t row) const {
+    const uint32_t n = re > rs ? re - rs : 0;
+    const uint32_t wend = (re + 127) & ~127u, ws = rs & ~127u, t = wend - re, a = t >> 2, b = t & 3;
+    const uint32_t J = n ? (wend - ws) >> 7 : 0, lead = rs - ws, m4 = n < 4 ? n : 4;
+    auto keep8 = [](int32_t d) -> uint64_t {
+      const uint32_t q = 4u * (uint32_t)(d < 0 ? 0 : (d > 8 ? 8 : d));
+      return (~0ull << q) << q;
+    };
+    uint32_t R = 0;
+    for (uint32_t p = 0; p < 16; ++p) {
+      const uint32_t col = (row * 16 + p) % 32;
+      const int32_t d0 = (int32_t)lead - (int32_t)(8 * p);
+      const uint64_t keep = keep8(d0), initm = keep & ~keep8(d0 + (int32_t)m4);
+      const int32_t x1 = (int32_t)(lead + m4) - 128;
+      const uint32_t m1 = (x1 > 0 && p == 0) ? (uint32_t)((1ull << (8 * x1)) - 1) : 0;
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t v = 2 * p + h;
+        const uint32_t nsl = J ? J - (v >= 32 - a ? 1 : 0) : 0;
+        uint32_t reg = 0;
+        for (uint32_t j = 0; j < nsl; ++j) {
+          uint64_t q;
+          memcpy(&q, &buf[ws + 8 * p + 128 * j], 8);
+          if (j == 0) q = (q & keep) ^ initm;
+          uint32_t x = (uint32_t)(q >> (32 * h));
+          if (j == 1 && v == 0) x ^= m1;
+          reg = U(reg ^ x, col);
+        }
+        if (J && b && v == 31 - a) {
+          const uint32_t junk = word(buf, (int64_t)ws + 128 * (J - 1) + 4 * v) & ~(uint32_t)(0xFFFFFFFFull >> (8 * b));
+          reg ^= U(junk, col);
+        }
+        R ^= F(reg, (v + a) & 31);
+      }
+    }
+    uint32_t T = 0;
+    for (uint32_t p = 0; p < 8; ++p) {
+      const uint32_t c = (row * 16 + p) % 32, nib = (R >> (4 * (p & 7))) & 15;
+      T ^= b ? rd(t_addr(c, 0, b, nib)) : nib << (4 * (p & 7));
+    }
+    R = n ? T : 0;
+    if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    return ~R;
+  }
   // CRC of frame [rs, re) of buf as row `row` of a wave would compute it.
   uint32_t crc(const std::vector<uint8_t>& buf, uint32_t rs, uint32_t re, uint32_t row) const {
     const uint32_t SB = 4 * RL;
@@ -176,6 +226,19 @@ int main() {
         ++checked;
         if (got != want && bad++ < 10)
           printf("RL=%d n=%u start=%u row=%u: got %08x want %08x\n", rl, n, start, row, got, want);
+      }
+    }
+  }
+  {  // lean line rows: the RL = 32 image, rows 0..3 of a wave
+    Emu e{32, build_lds_image(32u)};
+    for (uint32_t n = 0; n <= 1700; ++n) {
+      for (uint32_t start : {128u, 129u, 130u, 131u, 189u, 252u, 253u, 255u, 256u, 258u, 4221u}) {
+        if (start + n + 256 > buf.size()) continue;
+        const uint32_t row = (n + start) % 4;
+        const uint32_t got = e.crc32lean(buf, start, start + n, row);
+        const uint32_t want = ref_crc(&buf[start], n);
+        ++checked;
+        if (got != want && bad++ < 10) printf("lean n=%u start=%u row=%u: got %08x want %08x\n", n, start, row, got, want);
       }
     }
   }

@@ -75,7 +75,8 @@ def test_cpp_host_api_compiles_and_runs(tmp_path):
 def test_rows_kernel_algebra_emulated_on_cpu(tmp_path):
     """tests/cpp/rows_emulator.cpp: the CRC kernel's per-row algebra (window
     geometry, masks, junk removal, F, row XOR, Z_{-t}) replayed lane by lane on
-    the CPU from the library's real LDS images, for both row widths."""
+    the CPU from the library's real LDS images, for every row layout including
+    the lean line rows."""
     src = os.path.join(ROOT, "tests", "cpp", "rows_emulator.cpp")
     exe = tmp_path / "rows_emulator"
     subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", src, "-o", str(exe), "-L", os.path.dirname(L.LIB_PATH),
