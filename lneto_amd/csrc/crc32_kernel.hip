@@ -1089,8 +1089,8 @@ constexpr uint64_t kLineMean = 4096;
 // Lean line rows (lines_body) from kShortMean up to this mean frame length
 // (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
 constexpr uint64_t kLeanMean = 1600;
-template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 12, int S4 = 2,
-          int CHW = 4, int CH4 = 16, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
+template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
+          int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
           int KSL = 13>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
@@ -1304,6 +1304,12 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 23: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 8, 3, 4, 64); break;
       case 24: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 32); break;
       case 25: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 6, 3, 4, 64); break;
+      case 60: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 16, 2, 4, 16); break;  // longer 4-lane items
+      case 61: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 20, 1, 4, 16); break;
+      case 62: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 32); break;
+      case 63: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 16, 2, 4, 32); break;
+      case 64: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 64); break;
+      case 65: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 16, 2, 4, 64); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

@@ -22,10 +22,10 @@ pytestmark = pytest.mark.gpu
 # 17/21: forced one-word 16-lane rows, (KS, S) = (24, 1), (12, 3);
 # 18/19/28/29/40/41/42: forced two-word 16-lane rows (line windows, dwordx2 nt loads),
 #   (13, 1), (13, 2), (14, 1), (24, 1), (13, 1) with 8- and 16-frame chunks, (12, 2);
-# 22..25: forced 4-lane rows (16, 1), (8, 3), (12, 2), (6, 3);
+# 22..25, 60, 63: forced 4-lane rows (16, 2) with 32-frame chunks, (8, 3), (12, 2), (6, 3), (16, 2) with 16, (16, 2) with 32;
 # 50..52: forced lean line rows (lines_body), KSL = 13, 14, 12;
 # 56: the product dispatch with one-word 16-lane rows instead of lean rows
-FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56]
+FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 60, 63]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
