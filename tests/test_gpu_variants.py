@@ -66,3 +66,22 @@ def test_forced_configuration_parity(cuda, var):
         want = O.crc32_frames(data, off, threads=8)
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, f"{name}: variant {var} wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]})"
+
+
+@pytest.mark.parametrize("var", [0, 50, 18, 10])
+def test_range_end_alignments(cuda, var):
+    """The last frame of a workgroup's range ends at every offset mod 128: the
+    whole-line layouts load qwords / lines that straddle the end of the range
+    descriptor (rounded up to 4 bytes); the bytes inside must still count."""
+    import torch
+    for pad in range(0, 128, 1):
+        lens = np.array([1500, 1500, 1500, 1497 + (pad % 8)])
+        off = synth.offsets_from_lengths(lens) + pad
+        off = np.concatenate([[0], off]).astype(np.uint64)
+        n = len(off) - 1
+        data = synth.bytes_np(int(off[-1]), seed=pad)
+        d = torch.from_numpy(data).to(cuda)
+        o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+        got = _run(var, d, o, n)
+        want = O.crc32_frames(data, off)
+        assert np.array_equal(got, want), f"pad {pad}: variant {var} wrong at {np.nonzero(got != want)[0]}"
