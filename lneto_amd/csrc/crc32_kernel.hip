@@ -807,9 +807,16 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 //    first is chosen per row so that the 32 lanes of two rows always read 32
 //    distinct banks (rows 2m and 2m+1 differ in column parity).  One row XOR
 //    of the two F results, then Z_{-b}.
-template <CrcMode MODE, int KS, int VAR>
+//
+// WL = 1 runs the same slot structure on 32-lane rows (one dword per lane,
+// two frames per wave): lane p is virtual lane p, its register takes F from
+// column (p + a) mod 32, and the row XOR spans the 32 lanes.
+template <CrcMode MODE, int KS, int VAR, int WL = 2>
 __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
-  constexpr uint32_t CH = 4;  // frames per chunk = rows per wave
+  static_assert(WL == 1 || WL == 2, "words per lane");
+  constexpr uint32_t RL = 32 / WL;  // lanes per row
+  constexpr uint32_t CH = 64 / RL;  // frames per chunk = rows per wave
+  using Word = std::conditional_t<WL == 2, uint64_t, uint32_t>;
   static_assert(KS >= 4 && (KS - 1) * 128 <= 4095, "item shape");
   const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bt = L.bt;
   const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
@@ -853,13 +860,14 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     jmin = ~0u, jmax = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)J, 16 * r);
+      if ((uint32_t)r >= CH) break;
+      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)J, (int)RL * r);
       jmax = x > jmax ? x : jmax;
       jmin = x != 0 && x < jmin ? x : jmin;
     }
   };
 
-  uint64_t w[KS];
+  Word w[KS];
   uint32_t jk = 0;
   // runs of up to six step loads; a run no row of the wave reaches loads from
   // an out-of-range offset (no memory traffic).  Always issued: an asm load
@@ -868,15 +876,18 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   auto ld_runs = [&]<int K0>(auto self, std::integral_constant<int, K0>, uint32_t voff, uint32_t jmax) {
     if constexpr (K0 < KS - 1) {
       constexpr int N = KS - 1 - K0 < 6 ? KS - 1 - K0 : 6;
-      ld_run2<K0 * 128, N, 128>(w + K0, (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
+      if constexpr (WL == 2)
+        ld_run2<K0 * 128, N, 128>(w + K0, (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
+      else
+        ld_run<K0 * 128, N, 128, true>(w + K0, (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
       self(self, std::integral_constant<int, K0 + N>{}, voff, jmax);
     }
   };
   auto issue = [&](const Rowp& r) {
-    const uint32_t voff = r.J ? r.ws + p * 8u : kOOB;
+    const uint32_t voff = r.J ? r.ws + p * (4u * WL) : kOOB;
     if constexpr (VAR == 2) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) w[k] = (uint64_t)(voff * 0x9E3779B1u + k) * 0x100000001ull;
+      for (int k = 0; k < KS; ++k) w[k] = (Word)((uint64_t)(voff * 0x9E3779B1u + k) * 0x100000001ull);
     } else {
       uint32_t jmin, jmax;
       wave_min_max(r.J, jmin, jmax);
@@ -884,11 +895,14 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       // the last step from its own offset: out of range unless the frame has
       // KS lines (a 1500-B frame spans 12 lines at 29 % of start alignments;
       // the 13th line belongs to the next frame and would be fetched twice)
-      ld_run2<(KS - 1) * 128, 1, 128>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
+      if constexpr (WL == 2)
+        ld_run2<(KS - 1) * 128, 1, 128>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
+      else
+        ld_run<(KS - 1) * 128, 1, 128, true>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
     }
     // the word holding the frame end, when junk bytes follow it there: virtual lane 31 - a
     const uint32_t jl = 31u - (r.t >> 2);
-    const bool jn = r.J != 0 && p == (jl >> 1) && (r.t & 3u) != 0;
+    const bool jn = r.J != 0 && p == jl / WL && (r.t & 3u) != 0;
     jk = ld_buf<0>(jn ? r.ws + ((r.J - 1u) << 7) + (jl << 2) : kOOB, data_rsrc);
   };
 
@@ -906,42 +920,48 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       const uint32_t q = 4u * (uint32_t)(d < 0 ? 0 : (d > 8 ? 8 : d));
       return (~0ull << q) << q;
     };
-    const int32_t d0 = (int32_t)lead - (int32_t)(p << 3);
-    const uint64_t keep = keep8(d0), initm = keep & ~keep8(d0 + (int32_t)m4);
-    const uint64_t w0 = (w[0] & keep) ^ initm;
-    uint32_t nsl[2];
+    const int32_t d0 = (int32_t)lead - (int32_t)(p * 4u * WL);
+    Word w0;
+    if constexpr (WL == 2) {
+      const uint64_t keep = keep8(d0), initm = keep & ~keep8(d0 + (int32_t)m4);
+      w0 = (w[0] & keep) ^ initm;
+    } else {
+      const uint32_t keep = keep_from(d0), initm = keep & ~keep_from(d0 + (int32_t)m4);
+      w0 = (w[0] & keep) ^ initm;
+    }
+    uint32_t nsl[WL];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) nsl[h] = J ? J - (2u * p + h >= 32u - a ? 1u : 0u) : 0u;
+    for (int h = 0; h < WL; ++h) nsl[h] = J ? J - (WL * p + h >= 32u - a ? 1u : 0u) : 0u;
     const int32_t x1 = (int32_t)(lead + m4) - 128;  // init bytes spilling into step 1
     const uint32_t m1 = x1 > 0 && p == 0 ? (uint32_t)((1ull << (8 * x1)) - 1) : 0u;
     auto word = [&](int k, int h) -> uint32_t {
-      uint32_t x = (uint32_t)((k == 0 ? w0 : w[k]) >> (32 * h));
+      uint32_t x = (uint32_t)((uint64_t)(k == 0 ? w0 : w[k]) >> (32 * h));
       if (k == 1 && h == 0) x ^= m1;
       return x;
     };
-    uint32_t reg[2] = {0u, 0u};
+    uint32_t reg[WL] = {};
     if constexpr (VAR == 1) {
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) reg[h] ^= word(k, h);
+        for (int h = 0; h < WL; ++h) reg[h] ^= word(k, h);
     } else {
       // fast: every row's frame spans KS - 1 or KS lines (or none)
       const bool fast = !wave_any(J != 0 && J + 1u < (uint32_t)KS) && !wave_any(J > (uint32_t)KS);
       if (fast) {
-        uint32_t in[2];
+        uint32_t in[WL];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) in[h] = word(0, h);
+        for (int h = 0; h < WL; ++h) in[h] = word(0, h);
 #pragma unroll
         for (int k = 0; k < KS - 3; ++k)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) in[h] = u_step_xor(lds, in[h], word(k + 1, h), bu0, bu1);
+          for (int h = 0; h < WL; ++h) in[h] = u_step_xor(lds, in[h], word(k + 1, h), bu0, bu1);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) reg[h] = u_step_xor(lds, in[h], 0u, bu0, bu1);
+        for (int h = 0; h < WL; ++h) reg[h] = u_step_xor(lds, in[h], 0u, bu0, bu1);
 #pragma unroll
         for (int k = KS - 2; k < KS; ++k)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
+          for (int h = 0; h < WL; ++h) {
             const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
             reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
           }
@@ -956,10 +976,10 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
           if ((uint32_t)k >= jmax) continue;  // (no break: the loop must stay unrolled)
           if ((uint32_t)k + 1u < jmin) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) reg[h] = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
+            for (int h = 0; h < WL; ++h) reg[h] = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
           } else {
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
+            for (int h = 0; h < WL; ++h) {
               const uint32_t r2 = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
               reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
             }
@@ -972,17 +992,17 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
           // a separate array: reloading w here would give the ring registers
           // two definitions and hipcc copies between them at the loop head,
           // before the ring's wait
-          uint64_t wx[KX];
-          const uint32_t voff = j0 < J ? r.ws + (j0 << 7) + p * 8u : kOOB;
-          ld_item<0, KX, 128, true>(wx, voff, data_rsrc);
+          Word wx[KX];
+          const uint32_t voff = j0 < J ? r.ws + (j0 << 7) + p * (4u * WL) : kOOB;
+          ld_item<0, KX, 128, true>(wx, voff, data_rsrc);  // (uint32_t: ld_run nt, uint64_t: ld_run2)
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
           for (int k = 0; k < KX; ++k) asm volatile("" : "+v"(wx[k]));
 #pragma unroll
           for (int k = 0; k < KX; ++k)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const uint32_t r2 = u_step_xor(lds, reg[h] ^ (uint32_t)(wx[k] >> (32 * h)), 0u, bu0, bu1);
+            for (int h = 0; h < WL; ++h) {
+              const uint32_t r2 = u_step_xor(lds, reg[h] ^ (uint32_t)((uint64_t)wx[k] >> (32 * h)), 0u, bu0, bu1);
               reg[h] = j0 + (uint32_t)k < nsl[h] ? r2 : reg[h];
             }
         }
@@ -990,7 +1010,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     }
     Fin fin;
     fin.r0 = reg[0];
-    fin.r1 = reg[1];
+    fin.r1 = WL == 2 ? reg[WL - 1] : 0u;
     fin.junk = jk & ~(uint32_t)(0xFFFFFFFFull >> (8 * (t & 3u)));
     fin.f = r.f;
     fin.n = n;
@@ -1005,28 +1025,37 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   auto finish = [&](const Fin& fin) {
     const uint32_t n = fin.n, t = fin.t, a = t >> 2;
     const bool live = fin.f != kNoFrame;
-    uint32_t r0 = fin.r0, r1 = fin.r1;
-    if (wave_any(fin.junk != 0)) {
-      const uint32_t u = u_step(lds, fin.junk, bu0, bu1);
-      const bool odd = ((31u - a) & 1u) != 0;  // virtual lane 31 - a is register (31 - a) & 1
-      r0 ^= odd ? 0u : u;
-      r1 ^= odd ? u : 0u;
+    uint32_t R;
+    if constexpr (WL == 2) {
+      uint32_t r0 = fin.r0, r1 = fin.r1;
+      if (wave_any(fin.junk != 0)) {
+        const uint32_t u = u_step(lds, fin.junk, bu0, bu1);
+        const bool odd = ((31u - a) & 1u) != 0;  // virtual lane 31 - a is register (31 - a) & 1
+        r0 ^= odd ? 0u : u;
+        r1 ^= odd ? u : 0u;
+      }
+      // register h of lane p (virtual lane 2p + h) takes F_q, q = (2p + h + a) mod 32;
+      // the odd row of each pair goes first with the register whose column
+      // parity differs from the even row's
+      const auto as = __builtin_amdgcn_permlane16_swap(a, a, false, false);  // a of row 2m, of row 2m+1
+      const uint32_t hs = (row & 1u) ? (((as[0] ^ as[1]) & 1u) ^ 1u) : 0u;
+      const uint32_t x1 = hs ? r1 : r0, x2 = hs ? r0 : r1;
+      const uint32_t q1 = (2u * p + hs + a) & 31u, q2 = (2u * p + (hs ^ 1u) + a) & 31u;
+      const uint32_t F = f_step(lds, x1, kFBase | (q1 << 2)) ^ f_step(lds, x2, kFBase | (q2 << 2));
+      R = t_fix<16>(lds, row_xor<16>(F), t & 3u, p, bt);
+    } else {
+      // lane p (virtual lane p) takes F_q, q = (p + a) mod 32: 32 distinct
+      // columns per row, and the two rows sit in different halves of the wave
+      uint32_t r0 = fin.r0;
+      if (wave_any(fin.junk != 0)) r0 ^= u_step(lds, fin.junk, bu0, bu1);
+      R = t_fix<32>(lds, row_xor<32>(f_step(lds, r0, kFBase | (((p + a) & 31u) << 2))), t & 3u, p, bt);
     }
-    // register h of lane p (virtual lane 2p + h) takes F_q, q = (2p + h + a) mod 32;
-    // the odd row of each pair goes first with the register whose column
-    // parity differs from the even row's
-    const auto as = __builtin_amdgcn_permlane16_swap(a, a, false, false);  // a of row 2m, of row 2m+1
-    const uint32_t hs = (row & 1u) ? (((as[0] ^ as[1]) & 1u) ^ 1u) : 0u;
-    const uint32_t x1 = hs ? r1 : r0, x2 = hs ? r0 : r1;
-    const uint32_t q1 = (2u * p + hs + a) & 31u, q2 = (2u * p + (hs ^ 1u) + a) & 31u;
-    const uint32_t F = f_step(lds, x1, kFBase | (q1 << 2)) ^ f_step(lds, x2, kFBase | (q2 << 2));
-    uint32_t R = t_fix<16>(lds, row_xor<16>(F), t & 3u, p, bt);
     R = n != 0 ? R : 0u;
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
     const uint32_t crc = ~R;
     if (live && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
     pc += live ? 1u : 0u;
-    bool fl = wave_any(pc == 16u);
+    bool fl = wave_any(pc == RL);
     const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
     fl = fl || (now != win && wave_any(pc != 0));
     win = now;
@@ -1091,7 +1120,7 @@ constexpr uint64_t kLineMean = 4096;
 constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13>
+          int KSL = 13, int LWL = 2>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1227,8 +1256,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       L.p = lane & 3u, L.row = lane >> 2;
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
     } else if (rl == 16 && lean) {
-      L.p = lane & 15u, L.row = lane >> 4;
-      if constexpr (!SEG) lines_body<MODE, KSL, VAR>(lds, L, cx);
+      // lean rows: 16 lanes x two words (LWL = 2) or 32 lanes x one word (LWL = 1)
+      L.p = lane & (32u / LWL - 1u), L.row = lane / (32u / LWL);
+      if constexpr (!SEG) lines_body<MODE, KSL, VAR, LWL>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
       rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1>(lds, L, cx);
@@ -1296,6 +1326,10 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 52: LNX_LEAN(0, 12); break;
       case 53: LNX_LEAN(1, 13); break;
       case 54: LNX_LEAN(2, 13); break;
+      // forced lean rows on 32 lanes x one word (KSL 13), loads only, math only
+      case 70: LNX_LAUNCH(CrcMode::kCrc, 0, 16, 24, 1, 12, 2, 4, 16, false, 3, 24, 1, 4, 13, 1); break;
+      case 71: LNX_LAUNCH(CrcMode::kCrc, 1, 16, 24, 1, 12, 2, 4, 16, false, 3, 24, 1, 4, 13, 1); break;
+      case 72: LNX_LAUNCH(CrcMode::kCrc, 2, 16, 24, 1, 12, 2, 4, 16, false, 3, 24, 1, 4, 13, 1); break;
       // product dispatch with one-word 16-lane rows instead of lean rows (the r1f product)
       case 56: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 1); break;
 #undef LNX_LEAN

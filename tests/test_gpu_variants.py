@@ -24,8 +24,9 @@ pytestmark = pytest.mark.gpu
 #   (13, 1), (13, 2), (14, 1), (24, 1), (13, 1) with 8- and 16-frame chunks, (12, 2);
 # 22..25, 60, 63: forced 4-lane rows (16, 2) with 32-frame chunks, (8, 3), (12, 2), (6, 3), (16, 2) with 16, (16, 2) with 32;
 # 50..52: forced lean line rows (lines_body), KSL = 13, 14, 12;
-# 56: the product dispatch with one-word 16-lane rows instead of lean rows
-FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 60, 63]
+# 56: the product dispatch with one-word 16-lane rows instead of lean rows;
+# 70: forced lean rows on 32 lanes x one word
+FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 60, 63, 70]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -68,7 +69,7 @@ def test_forced_configuration_parity(cuda, var):
         assert bad.size == 0, f"{name}: variant {var} wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]})"
 
 
-@pytest.mark.parametrize("var", [0, 50, 18, 10])
+@pytest.mark.parametrize("var", [0, 50, 18, 10, 70])
 def test_range_end_alignments(cuda, var):
     """The last frame of a workgroup's range ends at every offset mod 128: the
     whole-line layouts load qwords / lines that straddle the end of the range
