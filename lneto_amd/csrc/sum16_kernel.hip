@@ -92,15 +92,16 @@ sum16_segments_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
 // aligned span, so every row instruction reads one whole line — the pattern
 // whose non-temporal streaming rate is 6.4-6.5 TB/s against 6.0 for the
 // 64-byte half lines above (DESIGN.md §3.1 "whole-line rows").  kLineUnroll
-// lines per row in flight.
-constexpr int kLineUnroll = 8;
+// lines per row in flight: 13 covers a 1500-B segment in one round trip
+// (6.24 TB/s against 6.07 with 8 and 6.19 with 16, tools/prof/sum16_variants.py).
+constexpr int kLineUnroll = 13;
 
 __device__ __forceinline__ uint64_t keep8(int32_t d) {  // bytes [d, 8) of a qword, d clamped to 0..8
   const uint32_t q = 4u * (uint32_t)(d < 0 ? 0 : (d > 8 ? 8 : d));
   return (~0ull << q) << q;
 }
 
-template <bool NT>
+template <bool NT, int UNR = kLineUnroll>
 __global__ void __launch_bounds__(kSumBlock)
 sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed, uint64_t nseg,
@@ -127,13 +128,13 @@ sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     uint32_t nlw = max(nl, (uint32_t)__shfl_xor((int)nl, 16));
     nlw = max(nlw, (uint32_t)__shfl_xor((int)nlw, 32));
     nlw = (uint32_t)__builtin_amdgcn_readfirstlane((int)nlw);
-    for (uint32_t k0 = 0; k0 < nlw; k0 += kLineUnroll) {
-      uint64_t x[kLineUnroll];
+    for (uint32_t k0 = 0; k0 < nlw; k0 += UNR) {
+      uint64_t x[UNR];
 #pragma unroll
-      for (int u = 0; u < kLineUnroll; ++u)
+      for (int u = 0; u < UNR; ++u)
         x[u] = k0 + u < nl ? (NT ? __builtin_nontemporal_load(base + 16u * (k0 + u)) : base[16u * (k0 + u)]) : 0ull;
 #pragma unroll
-      for (int u = 0; u < kLineUnroll; ++u) {
+      for (int u = 0; u < UNR; ++u) {
         const int32_t o0 = (int32_t)(128u * (k0 + u) + 8u * p) - (int32_t)mis;  // segment offset of byte 0
         const uint64_t y = x[u] & keep8(-o0) & ~keep8((int32_t)L - o0);
         E = __builtin_amdgcn_udot4((uint32_t)y, wE, E, false);
@@ -148,7 +149,8 @@ sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   }
 }
 
-// var 0: line rows (product); var 1: the half-line rows of sum16_segments_kernel; var 2: line rows, default cache policy
+// var 0: line rows (product); var 1: the half-line rows of sum16_segments_kernel; var 2: line rows, default cache
+// policy; var 3 / 4: line rows with 8 / 16 lines in flight
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                   const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                   hipStream_t stream, int var) {
@@ -159,6 +161,12 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
   if (grid > cap) grid = cap;
   if (var == 1)
     hipLaunchKernelGGL(sum16_segments_kernel, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
+                       off, len, seed, n, out);
+  else if (var == 3)
+    hipLaunchKernelGGL((sum16_lines_kernel<true, 8>), dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
+                       off, len, seed, n, out);
+  else if (var == 4)
+    hipLaunchKernelGGL((sum16_lines_kernel<true, 16>), dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
                        off, len, seed, n, out);
   else if (var == 2)
     hipLaunchKernelGGL(sum16_lines_kernel<false>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,

@@ -21,9 +21,9 @@ t0 = time.perf_counter()
 while time.perf_counter() - t0 < 0.5:
     launch(0)
 torch.cuda.synchronize()
-res = {0: [], 1: [], 2: []}
+res = {0: [], 1: [], 2: [], 3: [], 4: []}
 for r in range(reps):
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3, 4):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         e[0].record(s)
         for _ in range(20):
@@ -31,6 +31,6 @@ for r in range(reps):
         e[1].record(s)
         torch.cuda.synchronize()
         res[v].append(e[0].elapsed_time(e[1]) / 20)
-for v in (0, 1, 2):
+for v in (0, 1, 2, 3, 4):
     ms = float(np.median(res[v]))
     print(f"sum16 variant {v}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s  [{' '.join(f'{x:.4f}' for x in res[v])}]")
