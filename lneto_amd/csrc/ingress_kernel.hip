@@ -29,11 +29,15 @@
 // and the transport sum = pseudo-header addresses + transport segment.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace lnx {
 
 constexpr int kIngBlock = 256;
-constexpr int kIngUnroll = 8;  // dwords per lane in flight (512 B per row)
+// dwords per lane in flight: 24 (1536 B per row) reads a 1500-B frame in one
+// batch; 0.283 ms against 0.291 for 8 and 0.313 for 16 on 1 M x 1500 B
+// (bench.py --op ingress, LNX_PROF_INGRESS_UNROLL; profiles/r1g_ingress_unroll.txt)
+constexpr int kIngUnroll = 24;
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
 constexpr uint32_t kVerifyEvilBit = 1;
@@ -60,6 +64,7 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
   return (uint16_t)~(uint16_t)(sum + (sum >> 16));
 }
 
+template <int UNR>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
@@ -85,9 +90,9 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const int32_t kfend = (int32_t)((L + mis + 3) >> 2);         // dwords touching the frame
 
     // ---- first batch: dwords kstart + p + 16u; it also holds every header field
-    uint32_t x[kIngUnroll];
+    uint32_t x[UNR];
 #pragma unroll
-    for (int u = 0; u < kIngUnroll; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int32_t k = kstart + (int32_t)p + 16 * u;
       x[u] = L >= 14 && k < kfend ? base[k] : 0u;
     }
@@ -196,16 +201,16 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;  // bytes at even frame offsets
     const uint32_t wO = wE << 8 | wE >> 24;
     const int32_t ha = hdr_sum ? 14 : 0, hb = hdr_sum ? 34 : 0;
-    for (int32_t k0 = kstart + (int32_t)p; k0 < kend; k0 += 16 * kIngUnroll) {
+    for (int32_t k0 = kstart + (int32_t)p; k0 < kend; k0 += 16 * UNR) {
       if (k0 != kstart + (int32_t)p) {
 #pragma unroll
-        for (int u = 0; u < kIngUnroll; ++u) {
+        for (int u = 0; u < UNR; ++u) {
           const int32_t k = k0 + 16 * u;
           x[u] = k < kend ? base[k] : 0u;
         }
       }
 #pragma unroll
-      for (int u = 0; u < kIngUnroll; ++u) {
+      for (int u = 0; u < UNR; ++u) {
         const int32_t o0 = 4 * (k0 + 16 * u) - (int32_t)mis;
         const uint32_t xh = x[u] & range_mask(o0, ha, hb);
         const uint32_t xt = x[u] & (range_mask(o0, pa, pb) | range_mask(o0, la, lb));
@@ -231,8 +236,20 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
-  hipLaunchKernelGGL(ingress_verify_kernel, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n, flags,
-                     verdict, seg_len, trim);
+  // profiling: LNX_PROF_INGRESS_UNROLL=8|16 selects another batch depth
+  static const int unr = [] {
+    const char* e = getenv("LNX_PROF_INGRESS_UNROLL");
+    return e ? atoi(e) : kIngUnroll;
+  }();
+  if (unr == 8)
+    hipLaunchKernelGGL(ingress_verify_kernel<8>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n,
+                       flags, verdict, seg_len, trim);
+  else if (unr == 16)
+    hipLaunchKernelGGL(ingress_verify_kernel<16>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n,
+                       flags, verdict, seg_len, trim);
+  else
+    hipLaunchKernelGGL(ingress_verify_kernel<kIngUnroll>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
+                       off, n, flags, verdict, seg_len, trim);
   return hipGetLastError();
 }
 
