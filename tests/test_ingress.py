@@ -163,3 +163,34 @@ def test_gpu_header_sum_precedes_udp_size_checks(cuda, base_pad):
                                  torch.from_numpy(off.astype(np.int64)).to(cuda)).cpu().numpy()
     want = [O.ingress_verdict(f) for f in frames]
     assert got.tolist() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base_pad", [0, 5])
+def test_gpu_ingress_jumbo_frames(cuda, base_pad):
+    """Jumbo IPv4/IPv6 TCP and UDP frames (up to 9000 B: several batches of
+    lines per row), valid and with one corrupted payload byte each."""
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(31 + base_pad)
+    frames = []
+    for i in range(400):
+        n = int(rng.integers(1400, 8900))
+        pay = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        kind = i % 4
+        f = G.ether(0x0800, G.ipv4(6, G.tcp(pay))) if kind == 0 else \
+            G.ether(0x0800, G.ipv4(17, G.udp(pay))) if kind == 1 else \
+            G.ether(0x86DD, G.ipv6(6, G.tcp(pay))) if kind == 2 else G.ether(0x86DD, G.ipv6(17, G.udp(pay)))
+        if i % 3 == 0:
+            b = bytearray(f)
+            b[int(rng.integers(60, len(b)))] ^= 0x10
+            f = bytes(b)
+        frames.append(f)
+    data, off = _pack(frames, base_pad)
+    d = torch.from_numpy(data).to(cuda)
+    o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+    got = L.ingress_verify_batch(d, o).cpu().numpy()
+    want = np.array([O.ingress_verdict(f, 0) for f in frames], dtype=np.uint8)
+    assert (want == 3).sum() > 50 and (want == 0).sum() > 100
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
