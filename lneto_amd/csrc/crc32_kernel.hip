@@ -1361,6 +1361,10 @@ hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64
 }
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
+  // 80 / 81: the product with 2 / 4 workgroups per CU over the launch (one is
+  // resident at a time: the later ones go to the CUs that finish first)
+  if (var == 80 || var == 81)
+    return launch_rows(0, false, bytes, off, n, out, images, num_cus * (var == 80 ? 2 : 4), stream, nullptr);
   return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, timeline);
 }
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
