@@ -125,6 +125,84 @@ uint16_t oracle_payload_sum16(uint32_t sum, const uint8_t* p, size_t n) {
 /* crc.go:65-71 */
 uint16_t oracle_never_zero_sum(uint16_t s) { return s == 0 ? 0xffff : s; }
 
+/* ---- Go's amd64 fast path (CPU baseline only) -------------------------
+ * hash/crc32 on amd64 (crc32_amd64.go archUpdateIEEE) folds inputs of >= 64
+ * bytes with PCLMULQDQ (ieeeCLMUL in crc32_amd64.s: four 128-bit lanes folded
+ * by 512 bits, then by 128, then a Barrett reduction) over the largest
+ * multiple of 16 bytes, and finishes the 0..15 remaining bytes with
+ * slicing-by-8.  Restated here with the published folding constants of the
+ * reflected IEEE polynomial (x^(512+32), x^(512-32), x^(128+32), x^(128-32),
+ * x^64 mod P, P', mu), so the CPU baseline runs the algorithm lneto's Go
+ * build would; it is checked against the table form by tests/test_oracle.py. */
+#if defined(__x86_64__)
+#include <immintrin.h>
+__attribute__((target("pclmul,sse4.1"))) static uint32_t ieee_clmul(uint32_t crc, const uint8_t* buf, size_t len) {
+  /* len >= 64, len % 16 == 0; crc is the internal (inverted) register */
+  const __m128i k1k2 = _mm_set_epi64x(0x01c6e41596LL, 0x0154442bd4LL);
+  const __m128i k3k4 = _mm_set_epi64x(0x00ccaa009eLL, 0x01751997d0LL);
+  const __m128i k5k0 = _mm_set_epi64x(0, 0x0163cd6124LL);
+  const __m128i poly = _mm_set_epi64x(0x01f7011641LL, 0x01db710641LL);
+  __m128i x1 = _mm_loadu_si128((const __m128i*)(buf + 0x00));
+  __m128i x2 = _mm_loadu_si128((const __m128i*)(buf + 0x10));
+  __m128i x3 = _mm_loadu_si128((const __m128i*)(buf + 0x20));
+  __m128i x4 = _mm_loadu_si128((const __m128i*)(buf + 0x30));
+  x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128((int)crc));
+  buf += 64, len -= 64;
+  while (len >= 64) {
+    __m128i x5 = _mm_clmulepi64_si128(x1, k1k2, 0x00), x6 = _mm_clmulepi64_si128(x2, k1k2, 0x00);
+    __m128i x7 = _mm_clmulepi64_si128(x3, k1k2, 0x00), x8 = _mm_clmulepi64_si128(x4, k1k2, 0x00);
+    x1 = _mm_clmulepi64_si128(x1, k1k2, 0x11), x2 = _mm_clmulepi64_si128(x2, k1k2, 0x11);
+    x3 = _mm_clmulepi64_si128(x3, k1k2, 0x11), x4 = _mm_clmulepi64_si128(x4, k1k2, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x5), _mm_loadu_si128((const __m128i*)(buf + 0x00)));
+    x2 = _mm_xor_si128(_mm_xor_si128(x2, x6), _mm_loadu_si128((const __m128i*)(buf + 0x10)));
+    x3 = _mm_xor_si128(_mm_xor_si128(x3, x7), _mm_loadu_si128((const __m128i*)(buf + 0x20)));
+    x4 = _mm_xor_si128(_mm_xor_si128(x4, x8), _mm_loadu_si128((const __m128i*)(buf + 0x30)));
+    buf += 64, len -= 64;
+  }
+  __m128i x5;
+  x5 = _mm_clmulepi64_si128(x1, k3k4, 0x00), x1 = _mm_clmulepi64_si128(x1, k3k4, 0x11);
+  x1 = _mm_xor_si128(_mm_xor_si128(x1, x2), x5);
+  x5 = _mm_clmulepi64_si128(x1, k3k4, 0x00), x1 = _mm_clmulepi64_si128(x1, k3k4, 0x11);
+  x1 = _mm_xor_si128(_mm_xor_si128(x1, x3), x5);
+  x5 = _mm_clmulepi64_si128(x1, k3k4, 0x00), x1 = _mm_clmulepi64_si128(x1, k3k4, 0x11);
+  x1 = _mm_xor_si128(_mm_xor_si128(x1, x4), x5);
+  while (len >= 16) {
+    x2 = _mm_loadu_si128((const __m128i*)buf);
+    x5 = _mm_clmulepi64_si128(x1, k3k4, 0x00), x1 = _mm_clmulepi64_si128(x1, k3k4, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x2), x5);
+    buf += 16, len -= 16;
+  }
+  /* 128 -> 64 bits */
+  const __m128i m32 = _mm_setr_epi32(~0, 0, ~0, 0);
+  x2 = _mm_clmulepi64_si128(x1, k3k4, 0x10);
+  x1 = _mm_xor_si128(_mm_srli_si128(x1, 8), x2);
+  x2 = _mm_srli_si128(x1, 4);
+  x1 = _mm_clmulepi64_si128(_mm_and_si128(x1, m32), k5k0, 0x00);
+  x1 = _mm_xor_si128(x1, x2);
+  /* Barrett reduction to 32 bits */
+  x2 = _mm_clmulepi64_si128(_mm_and_si128(x1, m32), poly, 0x10);
+  x2 = _mm_clmulepi64_si128(_mm_and_si128(x2, m32), poly, 0x00);
+  x1 = _mm_xor_si128(x1, x2);
+  return (uint32_t)_mm_extract_epi32(x1, 1);
+}
+static int clmul_ok(void) { return __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1"); }
+#else
+static uint32_t ieee_clmul(uint32_t crc, const uint8_t* buf, size_t len) { (void)buf; (void)len; return crc; }
+static int clmul_ok(void) { return 0; }
+#endif
+
+int oracle_has_clmul(void) { return clmul_ok(); }
+
+/* crc32.Update(crc, IEEETable, p) as Go's amd64 build runs it (archUpdateIEEE) */
+uint32_t oracle_crc32_update_amd64(uint32_t crc, const uint8_t* p, size_t n) {
+  if (n >= 64 && clmul_ok()) {
+    const size_t done = n - (n & 15);
+    crc = ~ieee_clmul(~crc, p, done);
+    p += done, n -= done;
+  }
+  return n ? oracle_crc32_update(crc, p, n) : crc;
+}
+
 /* ---- batch helpers for the tests and the CPU baseline ----------------- */
 
 typedef struct {
@@ -132,13 +210,16 @@ typedef struct {
   const uint64_t* off;
   uint64_t lo, hi;
   uint32_t* out;
+  int amd64;
 } crc_job;
 
 static void* crc_worker(void* arg) {
   crc_job* j = (crc_job*)arg;
   for (uint64_t i = j->lo; i < j->hi; i++) {
     uint64_t s = j->off[i], e = j->off[i + 1];
-    j->out[i] = e > s ? oracle_crc32(j->bytes + s, (size_t)(e - s)) : 0;
+    j->out[i] = e <= s ? 0
+                : j->amd64 ? oracle_crc32_update_amd64(0, j->bytes + s, (size_t)(e - s))
+                           : oracle_crc32(j->bytes + s, (size_t)(e - s));
   }
   return NULL;
 }
@@ -146,8 +227,19 @@ static void* crc_worker(void* arg) {
 /* out[i] = CRC32(bytes[off[i]:off[i+1]]) with `threads` POSIX threads over
  * disjoint contiguous frame ranges (the "GOMAXPROCS goroutines each owning a
  * frame range" shape of BASELINE.md). */
+static int crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out, int threads,
+                        int amd64);
 int oracle_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out,
                         int threads) {
+  return crc32_frames(bytes, off, n, out, threads, 0);
+}
+/* the same with Go's amd64 fast path (CPU baseline) */
+int oracle_crc32_frames_amd64(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out,
+                              int threads) {
+  return crc32_frames(bytes, off, n, out, threads, 1);
+}
+static int crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t* out, int threads,
+                        int amd64) {
   ensure_tables();
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
@@ -161,6 +253,7 @@ int oracle_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, u
     jobs[t].lo = (uint64_t)t * per < n ? (uint64_t)t * per : n;
     jobs[t].hi = jobs[t].lo + per < n ? jobs[t].lo + per : n;
     jobs[t].out = out;
+    jobs[t].amd64 = amd64;
     if (threads == 1) {
       crc_worker(&jobs[t]);
     } else if (pthread_create(&th[t], NULL, crc_worker, &jobs[t]) == 0) {

@@ -316,6 +316,13 @@ def lib():
         L.oracle_crc32_frames.restype = ctypes.c_int
         L.oracle_crc32_frames.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                           ctypes.c_void_p, ctypes.c_int]
+        L.oracle_crc32_frames_amd64.restype = ctypes.c_int
+        L.oracle_crc32_frames_amd64.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.c_void_p, ctypes.c_int]
+        L.oracle_crc32_update_amd64.restype = ctypes.c_uint32
+        L.oracle_crc32_update_amd64.argtypes = [ctypes.c_uint32, u8p, ctypes.c_size_t]
+        L.oracle_has_clmul.restype = ctypes.c_int
+        L.oracle_has_clmul.argtypes = []
         L.oracle_sum16_segments.restype = None
         L.oracle_sum16_segments.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
@@ -344,14 +351,25 @@ def c_payload_sum16(seed: int, p: bytes) -> int:
     return lib().oracle_payload_sum16(seed, _u8p(p), len(p))
 
 
-def crc32_frames(data: np.ndarray, off: np.ndarray, threads: int = 1) -> np.ndarray:
-    """CRC32 of every frame data[off[i]:off[i+1]] (C oracle, `threads` threads)."""
+def crc32_frames(data: np.ndarray, off: np.ndarray, threads: int = 1, amd64: bool = False) -> np.ndarray:
+    """CRC32 of every frame data[off[i]:off[i+1]] (C oracle, `threads` threads).
+    amd64: Go's amd64 fast path (PCLMULQDQ folding + slicing-by-8 tail), the CPU
+    baseline's form; the table form otherwise."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     n = len(off) - 1
     out = np.zeros(max(n, 1), dtype=np.uint32)
-    lib().oracle_crc32_frames(data.ctypes.data, off.ctypes.data, n, out.ctypes.data, threads)
+    fn = lib().oracle_crc32_frames_amd64 if amd64 else lib().oracle_crc32_frames
+    fn(data.ctypes.data, off.ctypes.data, n, out.ctypes.data, threads)
     return out[:n]
+
+
+def has_clmul() -> bool:
+    return bool(lib().oracle_has_clmul())
+
+
+def c_crc32_update_amd64(crc: int, p: bytes) -> int:
+    return lib().oracle_crc32_update_amd64(crc, _u8p(p), len(p))
 
 
 def sum16_segments(data: np.ndarray, off: np.ndarray, length: np.ndarray,

@@ -131,3 +131,23 @@ def test_frames_batch_helper_threads():
     many = O.crc32_frames(data, off, threads=8)
     assert np.array_equal(one, many)
     assert all(int(one[i]) == O.crc32(data[int(off[i]):int(off[i + 1])].tobytes()) for i in range(0, 3000, 97))
+
+
+def test_amd64_fast_path_matches_table_form():
+    """Go's amd64 fast path restated (PCLMULQDQ folding for >= 64 bytes over the
+    largest multiple of 16, slicing-by-8 tail: crc32_amd64.go archUpdateIEEE)
+    equals the table form and zlib for every length 0..300, long random inputs
+    and any starting register; the CPU baseline runs this form."""
+    import zlib
+    if not O.has_clmul():
+        pytest.skip("no PCLMULQDQ on this CPU")
+    rng = np.random.default_rng(11)
+    lens = list(range(0, 301)) + [int(x) for x in rng.integers(301, 20000, size=100)]
+    for n in lens:
+        b = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        c = int(rng.integers(0, 1 << 32))
+        assert O.c_crc32_update_amd64(0, b) == zlib.crc32(b)
+        assert O.c_crc32_update_amd64(c, b) == zlib.crc32(b, c)
+    off = np.concatenate([[0], np.cumsum(rng.integers(0, 3000, size=500))]).astype(np.uint64)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    assert np.array_equal(O.crc32_frames(data, off, threads=4, amd64=True), O.crc32_frames(data, off, threads=4))
