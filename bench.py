@@ -73,6 +73,20 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
     from oracle import oracle as O
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
+    if op == "search":
+        # the C restatement of ethernet/crc.go:28-47 (crc32.Update per byte), one thread
+        nsamp = min(len(off_np) - 1, 256)
+        caps = [d_bytes[int(off_np[i]):int(off_np[i + 1])].cpu().numpy().tobytes() for i in range(nsamp)]
+        sb = sum(len(c) for c in caps)
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s / 2:
+            for c in caps:
+                O.c_crc32_search(c, 0)
+            reps += 1
+        el = time.perf_counter() - t0
+        return {"value": round(reps * sb / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "sample": f"{nsamp} captures x {frame_len} B; C restatement of ethernet/crc.go CRC32Search "
+                          "(one crc32.Update per byte), NOT lneto's Go binary"}
     if op == "sum16":
         threads = 1  # the C oracle's segment sum is single-threaded
     nsamp = min(len(off_np) - 1, 1 << 16)
@@ -163,7 +177,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
-    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress", "rx_ring"])
+    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress", "rx_ring", "search"])
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
@@ -228,6 +242,18 @@ def main():
         d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
     elif args.op == "fcs_verify":
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    elif args.op == "search":
+        # PIO-capture shape (phy/rmii.md:265-271): every capture is a frame whose
+        # LE FCS covers its first flen - 4 bytes, so CRC32Search scans it whole
+        # and finds flen - 4 (ethernet/crc.go:28-47)
+        if flen is None:
+            raise SystemExit("--op search needs fixed-size captures")
+        fr = d_bytes[: n_local * flen].view(n_local, flen)
+        starts = torch.arange(n_local, dtype=torch.int64, device=dev) * flen
+        lens = torch.full((n_local,), flen - 4, dtype=torch.int32, device=dev)
+        fcs = L.crc32_segments(d_bytes, starts, lens)
+        fr[:, flen - 4:] = fcs.view(torch.uint8).view(n_local, 4)
+        d_hit = torch.empty(n_local, dtype=torch.int64, device=dev)
     elif args.op == "ingress":
         if flen is None or flen < 42:
             raise SystemExit("--op ingress needs fixed-size frames of at least 42 bytes")
@@ -246,6 +272,8 @@ def main():
             L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "ingress":
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+        elif args.op == "search":
+            L.crc32_search_batch(d_bytes, d_off, out=d_hit, stream=stream)
         else:
             L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
 
@@ -301,6 +329,7 @@ def main():
         "fcs_verify": "GiB/s FCS verify (CRC-32 residue) over device-resident frames; % of HBM3E read peak",
         "sum16": "GiB/s RFC 791 internet checksum over device-resident segments; % of HBM3E read peak",
         "ingress": "GiB/s receive-path checksum verdicts (IPv4 header + UDP) over device-resident frames",
+        "search": "GiB/s CRC32Search over device-resident captures (bytes scanned to the FCS hit)",
     }[args.op]
     out = {
         "metric": metric,
@@ -334,7 +363,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
-                       "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel"}[args.op],
+                       "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
+                       "search": "lnx::crc32_search_kernel"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_launches": len(timed),
             "algorithmic_bytes_per_launch": nbytes,
@@ -356,6 +386,8 @@ def main():
             seeds = d_seed.cpu().numpy().view(np.uint32)
         elif args.op in ("fcs_verify", "ingress"):
             got = d_ok.cpu().numpy()
+        elif args.op == "search":
+            got = d_hit.cpu().numpy()
         else:
             got = d_crc.cpu().numpy().view(np.uint32)
         for i in idx:
@@ -367,6 +399,8 @@ def main():
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
             elif args.op == "ingress":
                 want = O.ingress_verdict(fr)
+            elif args.op == "search":
+                want = O.crc32_search(fr, 0)
             else:
                 want = O.crc32(fr)
             assert int(got[i]) == want, f"mismatch frame {i}"
