@@ -21,6 +21,7 @@
 // tables in LDS (shared; lookups here are rare next to the frame CRC path).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace lnx {
 
@@ -95,14 +96,131 @@ crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restric
   }
 }
 
+// ------------------------------------------------------------------ segment lanes (r1g)
+// One wave per capture, blocks of 64 x SEG bytes: lane j owns the SEG bytes
+// at block offset SEG*j and folds them twice with the byte-step table
+// (lane-private bank column, conflict-free):
+//   pass A, from 0, a word at a time (Z_4 tables): its local contribution
+//          l_j (lane 0 also folds in Z_SEG of the register carried in);
+//   scan:  P_j = XOR_{i<=j} Z_{SEG*(j-i)}(l_i) in six steps with the
+//          Z_{SEG*2^k} byte tables, so P_{j-1} is the register entering j;
+//   pass B, from P_{j-1}: the register after every byte, tested against the
+//          residue register as above.
+// About two table lookups per byte plus 28 per lane per block, against ten
+// per byte for the word-lane kernel above; bytes come from aligned dword loads
+// realigned with v_alignbyte (a dword holding a capture byte never crosses a
+// page, so loads stop at the capture end).
+constexpr uint32_t kSearchSeg = 32;
+constexpr uint32_t kSegTabOff = 256 + 6 * 1024;                  // after the word-lane kernel's tables
+constexpr uint32_t kSegTabDwords = 8192 + 7 * 1024;              // replicated byte table + 6 levels + Z_4
+constexpr int kSegBlock = 1024;  // 2 blocks per CU (57 KiB LDS each): 8 waves per SIMD
+
+__device__ __forceinline__ uint32_t zseg(const uint32_t* z, uint32_t x) {  // four byte tables at z
+  return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
+}
+
+__global__ void __launch_bounds__(kSegBlock)
+crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                        const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                        int64_t* __restrict__ result) {
+  constexpr uint32_t SEG = kSearchSeg, NW = SEG / 4;
+  __shared__ uint32_t lds[kSegTabDwords];
+  for (uint32_t i = threadIdx.x; i < kSegTabDwords; i += kSegBlock) lds[i] = tables[kSegTabOff + i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, col = lane & 31u;
+  const uint32_t* bt = lds + col;       // byte table, this lane's column: entry e at bt[32 e]
+  const uint32_t* zt = lds + 8192;      // level k at zt + 1024 k
+  auto bstep = [&](uint32_t r, uint32_t b) -> uint32_t { return bt[((r ^ b) & 0xFFu) << 5] ^ (r >> 8); };
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kSegBlock / 64);
+  for (uint64_t c = (uint64_t)blockIdx.x * (kSegBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
+    const uint64_t s = off[c], e = off[c + 1];
+    const int64_t L = e > s ? (int64_t)(e - s) : 0;
+    int64_t m = min_off ? min_off[c] : 0;
+    if (m < 0) m = 0;
+    int64_t found = -1;
+    if (L >= m + 4) {
+      const uint8_t* d = bytes + s;
+      uint32_t carry = 0xFFFFFFFFu;  // register entering the block (CRC init)
+      for (int64_t B = 0; B < L && found < 0; B += 64 * SEG) {
+        const int64_t base = B + (int64_t)(SEG * lane);
+        // the lane's SEG bytes: NW + 1 aligned dwords (only those holding a
+        // capture byte), realigned; bytes past the capture end read as junk
+        // and only feed states past it
+        const uintptr_t a = reinterpret_cast<uintptr_t>(d + base);
+        const uint32_t sh = (uint32_t)(a & 3u);
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
+        const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(d) + (uint64_t)L);  // first byte past the capture
+        uint32_t v[NW + 1];
+#pragma unroll
+        for (uint32_t i = 0; i <= NW; ++i)
+          v[i] = (int64_t)(a - sh + 4 * i) < lim ? wp[i] : 0u;
+        uint32_t u[NW];
+#pragma unroll
+        for (uint32_t i = 0; i < NW; ++i) u[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+        // pass A: only the segment's end state is needed, so whole words
+        // (slicing-by-4: Z_4 of register ^ word, shared tables)
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < NW; ++i) l = zseg(zt + 6 * 1024, l ^ u[i]);
+        if (lane == 0) l ^= zseg(zt, carry);
+        // scan: P holds lanes (lane - 2^k, lane] after step k
+        uint32_t P = l;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const uint32_t dd = 1u << k;
+          const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)P);
+          P ^= lane >= dd ? zseg(zt + 1024 * k, prev) : 0u;
+        }
+        uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P);
+        r = lane == 0 ? carry : r;
+        // pass B: the register after every byte; bit i of hm marks a residue
+        // after byte i, then the first bit whose offset is in range
+        uint32_t hm = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < SEG; ++i) {
+          r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
+          hm |= r == kResidueRegister ? (1u << i) : 0u;
+        }
+        // state after byte i is the CRC32Search candidate off = base + i + 1 - 4,
+        // valid for base + i + 1 in [m + 4, L]
+        const int64_t ilo = m + 3 - base, ihi = L - 1 - base;  // valid i range (inclusive)
+        if (ilo > 0) hm = ilo >= 32 ? 0u : hm & (0xFFFFFFFFu << ilo);
+        if (ihi < 31) hm = ihi < 0 ? 0u : hm & (0xFFFFFFFFu >> (31 - ihi));
+        const int64_t best = hm ? base + (int64_t)__builtin_ctz(hm) + 1 - 4 : -1;
+        const uint64_t hits = __builtin_amdgcn_ballot_w64(best >= 0);
+        if (hits) {
+          const uint32_t first = (uint32_t)__builtin_ctzll(hits);
+          found = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, first)) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)best >> 32), first) << 32));
+        }
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+      }
+    }
+    if (lane == 0) result[c] = found;
+  }
+}
+
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  uint64_t grid = (n + 3) / 4;
-  const uint64_t cap = (uint64_t)num_cus * 8;
-  if (grid > cap) grid = cap;
-  hipLaunchKernelGGL(crc32_search_kernel, dim3((unsigned)grid), dim3(kSearchBlock), 0, stream, bytes, off, min_off,
-                     n, tables, result);
+  // profiling: LNX_PROF_SEARCH=word selects the word-lane kernel
+  static const bool word = [] {
+    const char* e = getenv("LNX_PROF_SEARCH");
+    return e && e[0] == 'w';
+  }();
+  if (word) {
+    uint64_t grid = (n + 3) / 4;
+    const uint64_t cap = (uint64_t)num_cus * 8;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(crc32_search_kernel, dim3((unsigned)grid), dim3(kSearchBlock), 0, stream, bytes, off,
+                       min_off, n, tables, result);
+  } else {
+    uint64_t grid = (n + kSegBlock / 64 - 1) / (kSegBlock / 64);
+    const uint64_t cap = (uint64_t)num_cus * 2;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(crc32_search_seg_kernel, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
+                       min_off, n, tables, result);
+  }
   return hipGetLastError();
 }
 
