@@ -58,11 +58,11 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
 
 // Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
 // byte tables for k = 0..5 (search_kernel.hip).
-// Then the tables of crc32_search_seg_kernel (32-byte lane segments): the
+// Then the tables of crc32_search_seg_kernel (24-byte lane segments): the
 // byte-step table replicated in 32 bank columns (entry e, column c at 32e + c),
-// Z_{32*2^k} as four byte tables for k = 0..5, and Z_4 as four byte tables.
+// Z_{24*2^k} as four byte tables for k = 0..5, and Z_4 as four byte tables.
 std::vector<uint32_t> build_search_tables() {
-  constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 32;
+  constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 24;  // = kSearchSeg
   std::vector<uint32_t> t(kOld + 8192 + 7 * 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
   for (uint32_t k = 0; k < 6; ++k)

@@ -110,7 +110,7 @@ crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restric
 // per byte for the word-lane kernel above; bytes come from aligned dword loads
 // realigned with v_alignbyte (a dword holding a capture byte never crosses a
 // page, so loads stop at the capture end).
-constexpr uint32_t kSearchSeg = 32;
+constexpr uint32_t kSearchSeg = 24;  // 1536-byte blocks: a 1500-B capture keeps 63 of 64 lanes busy
 constexpr uint32_t kSegTabOff = 256 + 6 * 1024;                  // after the word-lane kernel's tables
 constexpr uint32_t kSegTabDwords = 8192 + 7 * 1024;              // replicated byte table + 6 levels + Z_4
 constexpr int kSegBlock = 1024;  // 2 blocks per CU (57 KiB LDS each): 8 waves per SIMD
@@ -119,7 +119,7 @@ __device__ __forceinline__ uint32_t zseg(const uint32_t* z, uint32_t x) {  // fo
   return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
 }
 
-__global__ void __launch_bounds__(kSegBlock)
+__global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
 crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
                         int64_t* __restrict__ result) {

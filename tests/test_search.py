@@ -53,3 +53,24 @@ def test_random_captures(cuda):
     want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
     bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
+
+
+def test_long_captures_many_blocks(cuda):
+    """Captures spanning several lane blocks (the register carried from block to
+    block), hits in any block, including on block boundaries."""
+    rng = np.random.default_rng(22)
+    caps, mins = [], []
+    for i in range(400):
+        n = int(rng.integers(1500, 12000))
+        body = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        if i % 4 == 3:  # FCS ending exactly on a multiple of 512 bytes
+            cut = max(0, (int(rng.integers(0, n)) // 512) * 512 - 4)
+        else:
+            cut = int(rng.integers(0, n + 1))
+        cap = body[:cut] + struct.pack("<I", O.crc32(body[:cut])) + body[cut:cut + int(rng.integers(0, 3000))]
+        caps.append(cap)
+        mins.append(int(rng.choice([0, 0, cut // 2, cut, cut + 1])))
+    got = _run(cuda, caps, mins)
+    want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
