@@ -38,6 +38,8 @@ constexpr int kIngBlock = 256;
 // batch; 0.283 ms against 0.291 for 8 and 0.313 for 16 on 1 M x 1500 B
 // (bench.py --op ingress, LNX_PROF_INGRESS_UNROLL; profiles/r1g_ingress_unroll.txt)
 constexpr int kIngUnroll = 24;
+// qword lanes (r1h product): 12 qwords per lane in flight, again 1536 B per row
+constexpr int kIngUnrollQ = 12;
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
 constexpr uint32_t kVerifyEvilBit = 1;
@@ -64,7 +66,10 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
   return (uint16_t)~(uint16_t)(sum + (sum >> 16));
 }
 
-template <int UNR>
+// QW: lanes load qwords (global_load_dwordx2: a 16-lane row reads a whole
+// 128-byte line per instruction), UNR qwords per lane in flight; otherwise
+// dwords (a 64-byte half line per row instruction), UNR dwords in flight
+template <int UNR, bool QW>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
@@ -83,25 +88,42 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const uint64_t len64 = e > s ? e - s : 0;
     const uint32_t L = len64 < 0x7FFFFFFFull ? (uint32_t)len64 : 0x7FFFFFFFu;
     const uint8_t* fr = bytes + s;
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 3u);
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & (QW ? 7u : 3u));
     const uint32_t* base = reinterpret_cast<const uint32_t*>(fr - mis);
     // dword k of base holds frame offsets 4k - mis .. 4k - mis + 3
     const int32_t kstart = (int32_t)((12 + mis) >> 2);          // dword holding frame offset 12
     const int32_t kfend = (int32_t)((L + mis + 3) >> 2);         // dwords touching the frame
 
-    // ---- first batch: dwords kstart + p + 16u; it also holds every header field
+    // ---- first batch: dwords kstart + p + 16u (QW: qwords qstart + p + 16u,
+    // qword Q = dwords 2Q, 2Q + 1); it also holds every header field
+    const uint2* base2 = reinterpret_cast<const uint2*>(base);
+    const int32_t qstart = kstart >> 1, qfend = (kfend + 1) >> 1;
     uint32_t x[UNR];
+    uint2 y[QW ? UNR : 1];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int32_t k = kstart + (int32_t)p + 16 * u;
-      x[u] = L >= 14 && k < kfend ? base[k] : 0u;
+      if constexpr (QW) {
+        const int32_t q = qstart + (int32_t)p + 16 * u;
+        y[u] = L >= 14 && q < qfend ? base2[q] : make_uint2(0u, 0u);
+      } else {
+        const int32_t k = kstart + (int32_t)p + 16 * u;
+        x[u] = L >= 14 && k < kfend ? base[k] : 0u;
+      }
     }
-    // dword kstart + kk of this row (kk < 32) from the lane that loaded it
+    // dword kstart + kk of this row (kk < 31) from the lane that loaded it
     auto rowword = [&](int32_t kk) -> uint32_t {
-      const int addr = (int)((row * 16u + ((uint32_t)kk & 15u)) * 4u);
-      const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[0]);
-      const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[1]);
-      return kk < 16 ? a : b;
+      if constexpr (QW) {
+        const uint32_t rel = (uint32_t)(kstart - 2 * qstart + kk);  // dword of the row's first qword batch
+        const int addr = (int)((row * 16u + ((rel >> 1) & 15u)) * 4u);
+        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)y[0].x);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)y[0].y);
+        return (rel & 1u) ? b : a;
+      } else {
+        const int addr = (int)((row * 16u + ((uint32_t)kk & 15u)) * 4u);
+        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[0]);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)x[1]);
+        return kk < 16 ? a : b;
+      }
     };
     const uint32_t sh = (12 + mis) & 3u;  // byte of frame offset 12 inside dword kstart
     const uint32_t w0 = rowword(0), w1 = rowword(1), w2 = rowword(2), w3 = rowword(3);
@@ -201,7 +223,46 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const uint32_t wE = (mis & 1u) ? 0x01000100u : 0x00010001u;  // bytes at even frame offsets
     const uint32_t wO = wE << 8 | wE >> 24;
     const int32_t ha = hdr_sum ? 14 : 0, hb = hdr_sum ? 34 : 0;
-    for (int32_t k0 = kstart + (int32_t)p; k0 < kend; k0 += 16 * UNR) {
+    if constexpr (QW) {
+      // Only the first qword of the first batch can hold header, pseudo-header
+      // or transport-start bytes: every later qword starts at frame offset
+      // >= 8 * (qstart + 16) - mis >= 126, past hb = 34, pb <= 54 and
+      // la <= 74. There the transport mask is the end bound alone and the
+      // header sum takes nothing.
+      const int32_t qend = (kend + 1) >> 1;
+      bool first = true;
+      for (int32_t q0 = qstart + (int32_t)p; q0 < qend; q0 += 16 * UNR) {
+        if (!first) {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const int32_t q = q0 + 16 * u;
+            y[u] = q < qend ? base2[q] : make_uint2(0u, 0u);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t w = h ? y[u].y : y[u].x;
+            const int32_t o0 = 4 * (2 * (q0 + 16 * u) + h) - (int32_t)mis;
+            if (u == 0 && first) {
+              const uint32_t xh = w & range_mask(o0, ha, hb);
+              const uint32_t xt = w & (range_mask(o0, pa, pb) | range_mask(o0, la, lb));
+              hE = __builtin_amdgcn_udot4(xh, wE, hE, false);
+              hO = __builtin_amdgcn_udot4(xh, wO, hO, false);
+              tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
+              tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
+            } else {
+              const uint32_t xt = w & ~ing_keep_from(lb - o0);
+              tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
+              tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
+            }
+          }
+        }
+        first = false;
+      }
+    }
+    for (int32_t k0 = kstart + (int32_t)p; !QW && k0 < kend; k0 += 16 * UNR) {
       if (k0 != kstart + (int32_t)p) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
@@ -236,20 +297,24 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   const uint64_t cap = (uint64_t)num_cus * 32;
   if (grid > cap) grid = cap;
-  // profiling: LNX_PROF_INGRESS_UNROLL=8|16 selects another batch depth
+  // profiling: LNX_PROF_INGRESS_UNROLL=8|16|24 selects the dword-lane form
+  // with that batch depth (24 = the r1g product)
   static const int unr = [] {
     const char* e = getenv("LNX_PROF_INGRESS_UNROLL");
-    return e ? atoi(e) : kIngUnroll;
+    return e ? atoi(e) : 0;
   }();
   if (unr == 8)
-    hipLaunchKernelGGL(ingress_verify_kernel<8>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n,
-                       flags, verdict, seg_len, trim);
-  else if (unr == 16)
-    hipLaunchKernelGGL(ingress_verify_kernel<16>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes, off, n,
-                       flags, verdict, seg_len, trim);
-  else
-    hipLaunchKernelGGL(ingress_verify_kernel<kIngUnroll>, dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
+    hipLaunchKernelGGL((ingress_verify_kernel<8, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
                        off, n, flags, verdict, seg_len, trim);
+  else if (unr == 16)
+    hipLaunchKernelGGL((ingress_verify_kernel<16, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
+                       off, n, flags, verdict, seg_len, trim);
+  else if (unr == kIngUnroll)
+    hipLaunchKernelGGL((ingress_verify_kernel<kIngUnroll, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
+                       off, n, flags, verdict, seg_len, trim);
+  else
+    hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream,
+                       bytes, off, n, flags, verdict, seg_len, trim);
   return hipGetLastError();
 }
 
