@@ -1,0 +1,107 @@
+"""CPU emulation of crc32_search_seg_kernel's algebra (lneto_amd/csrc/search_kernel.hip).
+
+The kernel answers ethernet.CRC32Search (ethernet/crc.go:28-47) for one
+capture per wave, in blocks of 64 lane segments of SEG bytes:
+  pass A  l_j  = segment j folded from register 0 (lane 0 also Z_SEG(carry)),
+  scan    P_j  = XOR_{i<=j} Z_{SEG*(j-i)}(l_i) by six doubling steps with the
+               Z_{SEG*2^k} tables,
+  pass B  from P_{j-1} (lane 0: the carry) the register after every byte,
+          tested against the residue register 0xDEBB20E3.
+This restates that schedule in Python, with the kernel's segment size and its
+treatment of bytes past the capture end, and checks it against the
+Go-semantics oracle. It pins the scan identity and the block carry on the CPU;
+tests/test_search.py checks the kernel itself on the GPU.
+"""
+import struct
+
+import numpy as np
+
+from oracle import oracle as O
+
+SEG = 24          # kSearchSeg
+LANES = 64
+RESIDUE = 0xDEBB20E3
+
+_T = []
+for _e in range(256):
+    _c = _e
+    for _ in range(8):
+        _c = (_c >> 1) ^ (0xEDB88320 if _c & 1 else 0)
+    _T.append(_c)
+
+
+def _byte_step(r, b):
+    return _T[(r ^ b) & 0xFF] ^ (r >> 8)
+
+
+def _zshift(x, nbytes):
+    """Z_n: the register after n zero bytes from register x (linear in x)."""
+    for _ in range(nbytes):
+        x = _byte_step(x, 0)
+    return x
+
+
+def _zshift_table(nbytes):
+    """Z_n through its four byte tables, as the kernel's LDS image holds it."""
+    tabs = [[_zshift(e << (8 * m), nbytes) for e in range(256)] for m in range(4)]
+    return lambda x: tabs[0][x & 0xFF] ^ tabs[1][(x >> 8) & 0xFF] ^ tabs[2][(x >> 16) & 0xFF] ^ tabs[3][x >> 24]
+
+
+_Z4 = _zshift_table(4)
+_ZLEVEL = [_zshift_table(SEG << k) for k in range(6)]
+
+
+def seg_search(data: bytes, min_off: int) -> int:
+    L = len(data)
+    m = max(min_off, 0)
+    if L < m + 4:
+        return -1
+    carry = 0xFFFFFFFF
+    for B in range(0, L, LANES * SEG):
+        segs = []
+        for j in range(LANES):
+            seg = data[B + SEG * j: B + SEG * (j + 1)]
+            segs.append(seg + bytes(SEG - len(seg)))   # past the end: any bytes (zeros here)
+        # pass A, a word at a time with Z_4
+        l = []
+        for j, seg in enumerate(segs):
+            v = 0
+            for w in struct.unpack("<%dI" % (SEG // 4), seg):
+                v = _Z4(v ^ w)
+            if j == 0:
+                v ^= _ZLEVEL[0](carry)
+            l.append(v)
+        # scan: P holds lanes (j - 2^k, j] after step k
+        P = list(l)
+        for k in range(6):
+            d = 1 << k
+            P = [P[j] ^ (_ZLEVEL[k](P[j - d]) if j >= d else 0) for j in range(LANES)]
+        # pass B: first valid hit in (lane, byte) order
+        for j, seg in enumerate(segs):
+            r = carry if j == 0 else P[j - 1]
+            base = B + SEG * j
+            for i, b in enumerate(seg):
+                r = _byte_step(r, b)
+                k = base + i + 1   # bytes consumed
+                if r == RESIDUE and m + 4 <= k <= L:
+                    return k - 4
+        carry = P[LANES - 1]
+    return -1
+
+
+def test_seg_schedule_matches_oracle():
+    rng = np.random.default_rng(31)
+    cases = []
+    for n in [0, 3, 4, 5, 23, 24, 25, 1499, 1536, 1537, 3100]:
+        body = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        cases.append((body, 0))
+        cases.append((body + struct.pack("<I", O.crc32(body)), 0))
+        cases.append((body + struct.pack("<I", O.crc32(body)) + body[:40], n))
+        cases.append((body + struct.pack("<I", O.crc32(body)) + body[:40], n + 1))
+    cases.append((b"\0\0\0\0" + bytes(100), 0))
+    # hits straddling lane segments and the 1536-byte block edge
+    for cut in [20, 21, 22, 23, 44, 1532, 1533, 1534, 1535, 1536, 3068]:
+        body = rng.integers(0, 256, size=cut, dtype=np.uint8).tobytes()
+        cases.append((body + struct.pack("<I", O.crc32(body)) + bytes(9), 0))
+    for data, mo in cases:
+        assert seg_search(data, mo) == O.crc32_search(data, mo), (len(data), mo)
