@@ -119,6 +119,10 @@ __device__ __forceinline__ uint32_t zseg(const uint32_t* z, uint32_t x) {  // fo
   return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
 }
 
+// kBallot: pass B tests each byte with one compare into a wave mask and keeps
+// the first (lane, byte) hit in scalar registers (a residue hit is rare: the
+// branch is taken about once per capture); otherwise a per-lane hit bitmask
+template <bool kBallot>
 __global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
 crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
@@ -150,10 +154,13 @@ crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __res
         const uint32_t sh = (uint32_t)(a & 3u);
         const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
         const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(d) + (uint64_t)L);  // first byte past the capture
+        // dwords of the lane window that hold a capture byte (a 32-bit count,
+        // so each load's guard is one 32-bit compare)
+        const int64_t nd64 = (lim - (int64_t)(a - sh) + 3) >> 2;
+        const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
         uint32_t v[NW + 1];
 #pragma unroll
-        for (uint32_t i = 0; i <= NW; ++i)
-          v[i] = (int64_t)(a - sh + 4 * i) < lim ? wp[i] : 0u;
+        for (uint32_t i = 0; i <= NW; ++i) v[i] = (int32_t)i < nd ? wp[i] : 0u;
         uint32_t u[NW];
 #pragma unroll
         for (uint32_t i = 0; i < NW; ++i) u[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
@@ -173,25 +180,43 @@ crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __res
         }
         uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P);
         r = lane == 0 ? carry : r;
-        // pass B: the register after every byte; bit i of hm marks a residue
-        // after byte i, then the first bit whose offset is in range
-        uint32_t hm = 0;
+        // pass B: the register after every byte. The state after byte i is the
+        // CRC32Search candidate off = base + i + 1 - 4, valid for
+        // base + i + 1 in [m + 4, L]
+        if (kBallot) {
+          uint32_t best_lane = 64, best_i = 0;  // wave-uniform
 #pragma unroll
-        for (uint32_t i = 0; i < SEG; ++i) {
-          r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
-          hm |= r == kResidueRegister ? (1u << i) : 0u;
-        }
-        // state after byte i is the CRC32Search candidate off = base + i + 1 - 4,
-        // valid for base + i + 1 in [m + 4, L]
-        const int64_t ilo = m + 3 - base, ihi = L - 1 - base;  // valid i range (inclusive)
-        if (ilo > 0) hm = ilo >= 32 ? 0u : hm & (0xFFFFFFFFu << ilo);
-        if (ihi < 31) hm = ihi < 0 ? 0u : hm & (0xFFFFFFFFu >> (31 - ihi));
-        const int64_t best = hm ? base + (int64_t)__builtin_ctz(hm) + 1 - 4 : -1;
-        const uint64_t hits = __builtin_amdgcn_ballot_w64(best >= 0);
-        if (hits) {
-          const uint32_t first = (uint32_t)__builtin_ctzll(hits);
-          found = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, first)) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)best >> 32), first) << 32));
+          for (uint32_t i = 0; i < SEG; ++i) {
+            r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
+            if (__builtin_amdgcn_ballot_w64(r == kResidueRegister)) {
+              const int64_t k = base + (int64_t)i + 1;
+              const uint64_t ok = __builtin_amdgcn_ballot_w64(r == kResidueRegister && k >= m + 4 && k <= L);
+              if (ok) {
+                const uint32_t ln = (uint32_t)__builtin_ctzll(ok);
+                if (ln < best_lane) best_lane = ln, best_i = i;
+              }
+            }
+          }
+          if (best_lane < 64) found = B + (int64_t)(SEG * best_lane + best_i) + 1 - 4;
+        } else {
+          // bit i of hm marks a residue after byte i, then the first bit whose
+          // offset is in range
+          uint32_t hm = 0;
+#pragma unroll
+          for (uint32_t i = 0; i < SEG; ++i) {
+            r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
+            hm |= r == kResidueRegister ? (1u << i) : 0u;
+          }
+          const int64_t ilo = m + 3 - base, ihi = L - 1 - base;  // valid i range (inclusive)
+          if (ilo > 0) hm = ilo >= 32 ? 0u : hm & (0xFFFFFFFFu << ilo);
+          if (ihi < 31) hm = ihi < 0 ? 0u : hm & (0xFFFFFFFFu >> (31 - ihi));
+          const int64_t best = hm ? base + (int64_t)__builtin_ctz(hm) + 1 - 4 : -1;
+          const uint64_t hits = __builtin_amdgcn_ballot_w64(best >= 0);
+          if (hits) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(hits);
+            found = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, first)) |
+                              ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)best >> 32), first) << 32));
+          }
         }
         carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
       }
@@ -204,11 +229,12 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // profiling: LNX_PROF_SEARCH=word selects the word-lane kernel
-  static const bool word = [] {
+  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B
+  static const char mode = [] {
     const char* e = getenv("LNX_PROF_SEARCH");
-    return e && e[0] == 'w';
+    return e ? e[0] : '\0';
   }();
-  if (word) {
+  if (mode == 'w') {
     uint64_t grid = (n + 3) / 4;
     const uint64_t cap = (uint64_t)num_cus * 8;
     if (grid > cap) grid = cap;
@@ -218,8 +244,12 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
     uint64_t grid = (n + kSegBlock / 64 - 1) / (kSegBlock / 64);
     const uint64_t cap = (uint64_t)num_cus * 2;
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(crc32_search_seg_kernel, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
-                       min_off, n, tables, result);
+    if (mode == 'h')  // per-lane hit bitmask (r1h before the ballot form)
+      hipLaunchKernelGGL(crc32_search_seg_kernel<false>, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
+                         min_off, n, tables, result);
+    else
+      hipLaunchKernelGGL(crc32_search_seg_kernel<true>, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
+                         min_off, n, tables, result);
   }
   return hipGetLastError();
 }
