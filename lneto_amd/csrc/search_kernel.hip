@@ -122,7 +122,12 @@ __device__ __forceinline__ uint32_t zseg(const uint32_t* z, uint32_t x) {  // fo
 // kBallot: pass B tests each byte with one compare into a wave mask and keeps
 // the first (lane, byte) hit in scalar registers (a residue hit is rare: the
 // branch is taken about once per capture); otherwise a per-lane hit bitmask
-template <bool kBallot>
+// kZWords: pass A folds its first kZWords words through the shared Z_4 tables
+// (fewer VALU, bank conflicts) and the rest byte by byte through the
+// conflict-free byte column (more VALU, no conflicts); 2 of 6 balances the two
+// (r1h: 0.798 ms against 0.834 for 6, 0.804 for 3, 0.811 for 1, 0.814 for 0)
+constexpr int kSearchZWords = 2;
+template <bool kBallot, int kZWords>
 __global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
 crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
@@ -168,7 +173,14 @@ crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __res
         // (slicing-by-4: Z_4 of register ^ word, shared tables)
         uint32_t l = 0;
 #pragma unroll
-        for (uint32_t i = 0; i < NW; ++i) l = zseg(zt + 6 * 1024, l ^ u[i]);
+        for (uint32_t i = 0; i < NW; ++i) {
+          if ((int)i < kZWords) {
+            l = zseg(zt + 6 * 1024, l ^ u[i]);
+          } else {  // the same map through the conflict-free byte column
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) l = bstep(l, u[i] >> (8 * q));
+          }
+        }
         if (lane == 0) l ^= zseg(zt, carry);
         // scan: P holds lanes (lane - 2^k, lane] after step k
         uint32_t P = l;
@@ -229,7 +241,7 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // profiling: LNX_PROF_SEARCH=word selects the word-lane kernel
-  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B
+  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B, =6 pass A all by Z_4
   static const char mode = [] {
     const char* e = getenv("LNX_PROF_SEARCH");
     return e ? e[0] : '\0';
@@ -244,12 +256,15 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
     uint64_t grid = (n + kSegBlock / 64 - 1) / (kSegBlock / 64);
     const uint64_t cap = (uint64_t)num_cus * 2;
     if (grid > cap) grid = cap;
-    if (mode == 'h')  // per-lane hit bitmask (r1h before the ballot form)
-      hipLaunchKernelGGL(crc32_search_seg_kernel<false>, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
-                         min_off, n, tables, result);
+    if (mode == 'h')  // per-lane hit bitmask, pass A all Z_4 (r1h before the ballot form)
+      hipLaunchKernelGGL((crc32_search_seg_kernel<false, 6>), dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes,
+                         off, min_off, n, tables, result);
+    else if (mode == '6')  // pass A all Z_4
+      hipLaunchKernelGGL((crc32_search_seg_kernel<true, 6>), dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes,
+                         off, min_off, n, tables, result);
     else
-      hipLaunchKernelGGL(crc32_search_seg_kernel<true>, dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes, off,
-                         min_off, n, tables, result);
+      hipLaunchKernelGGL((crc32_search_seg_kernel<true, kSearchZWords>), dim3((unsigned)grid), dim3(kSegBlock), 0,
+                         stream, bytes, off, min_off, n, tables, result);
   }
   return hipGetLastError();
 }

@@ -3,6 +3,7 @@
 The kernel answers ethernet.CRC32Search (ethernet/crc.go:28-47) for one
 capture per wave, in blocks of 64 lane segments of SEG bytes:
   pass A  l_j  = segment j folded from register 0 (lane 0 also Z_SEG(carry)),
+          its first kSearchZWords words through Z_4, the rest byte by byte,
   scan    P_j  = XOR_{i<=j} Z_{SEG*(j-i)}(l_i) by six doubling steps with the
                Z_{SEG*2^k} tables,
   pass B  from P_{j-1} (lane 0: the carry) the register after every byte,
@@ -19,6 +20,7 @@ import numpy as np
 from oracle import oracle as O
 
 SEG = 24          # kSearchSeg
+KZ = 2            # kSearchZWords
 LANES = 64
 RESIDUE = 0xDEBB20E3
 
@@ -62,12 +64,16 @@ def seg_search(data: bytes, min_off: int) -> int:
         for j in range(LANES):
             seg = data[B + SEG * j: B + SEG * (j + 1)]
             segs.append(seg + bytes(SEG - len(seg)))   # past the end: any bytes (zeros here)
-        # pass A, a word at a time with Z_4
+        # pass A: the first KZ words with Z_4, the rest byte by byte
         l = []
         for j, seg in enumerate(segs):
             v = 0
-            for w in struct.unpack("<%dI" % (SEG // 4), seg):
-                v = _Z4(v ^ w)
+            for wi, w in enumerate(struct.unpack("<%dI" % (SEG // 4), seg)):
+                if wi < KZ:
+                    v = _Z4(v ^ w)
+                else:
+                    for q in range(4):
+                        v = _byte_step(v, (w >> (8 * q)) & 0xFF)
             if j == 0:
                 v ^= _ZLEVEL[0](carry)
             l.append(v)
