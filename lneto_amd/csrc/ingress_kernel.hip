@@ -295,7 +295,15 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   if (n == 0) return hipSuccess;
   const uint64_t frames_per_block = (kIngBlock / 64) * 4;
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
-  const uint64_t cap = (uint64_t)num_cus * 32;
+  // 128 workgroups per CU (2 passes of 16 frames each at 1 M frames): 0.2594 ms against
+  // 0.272 for 32, 0.2645 for 256 (profiles/r1h_grid_sweep.txt).
+  // profiling: LNX_PROF_INGRESS_WG_PER_CU overrides it
+  static const uint64_t wg_per_cu = [] {
+    const char* e = getenv("LNX_PROF_INGRESS_WG_PER_CU");
+    const int v = e ? atoi(e) : 0;
+    return (uint64_t)(v > 0 ? v : 128);
+  }();
+  const uint64_t cap = (uint64_t)num_cus * wg_per_cu;
   if (grid > cap) grid = cap;
   // profiling: LNX_PROF_INGRESS_UNROLL=8|16|24 selects the dword-lane form
   // with that batch depth (24 = the r1g product)

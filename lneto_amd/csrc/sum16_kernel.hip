@@ -16,6 +16,7 @@
 // v_dot4_u32_u8 forms the even/odd byte sums, DPP adds reduce the row.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace lnx {
 
@@ -157,7 +158,15 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
   if (n == 0) return hipSuccess;
   const uint64_t seg_per_block = kSumWaves * 4;
   uint64_t grid = (n + seg_per_block - 1) / seg_per_block;
-  const uint64_t cap = (uint64_t)num_cus * 32;
+  // 256 workgroups per CU (one pass of 16 segments each at 1 M segments): 0.237-0.240 ms
+  // against 0.259 for 32, 0.248 for 128 (profiles/r1h_grid_sweep.txt).
+  // profiling: LNX_PROF_SUM16_WG_PER_CU overrides it
+  static const uint64_t wg_per_cu = [] {
+    const char* e = getenv("LNX_PROF_SUM16_WG_PER_CU");
+    const int v = e ? atoi(e) : 0;
+    return (uint64_t)(v > 0 ? v : 256);
+  }();
+  const uint64_t cap = (uint64_t)num_cus * wg_per_cu;
   if (grid > cap) grid = cap;
   if (var == 1)
     hipLaunchKernelGGL(sum16_segments_kernel, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes,
