@@ -171,17 +171,77 @@ class CRC791:
 
 
 # ------------------------------------------------------- batched (device)
-def _stream_ptr(stream):
+def _dtypes(*names):
     import torch
-    if stream is None:
-        stream = torch.cuda.current_stream()
-    return stream.cuda_stream
+    table = {
+        "u8": (torch.uint8, torch.int8),
+        "i16": (torch.int16, getattr(torch, "uint16", torch.int16)),
+        "i32": (torch.int32, getattr(torch, "uint32", torch.int32)),
+        "i64": (torch.int64, getattr(torch, "uint64", torch.int64)),
+    }
+    return [table[n] for n in names]
 
 
-def _dev_check(*tensors):
-    for t in tensors:
-        if t is not None and (not t.is_cuda or not t.is_contiguous()):
-            raise LnetoError("batch arguments must be contiguous device tensors")
+class _Batch:
+    """Argument check and device scope of one batch call.
+
+    Every tensor must be a contiguous device tensor of the 8-, 16-, 32- or 64-bit
+    width the C-ABI reads through it (signedness is free: the kernels see the
+    bits), and all of them must live on ONE device.  The call then runs with that
+    device current and on its stream (the caller's ``stream`` must be on the same
+    device), so the library's per-device context and the kernel's memory agree.
+    """
+
+    def __init__(self, what, args, stream):
+        import torch
+        self.what = what
+        dev = None
+        for name, t, kind in args:
+            if t is None:
+                continue
+            if not isinstance(t, torch.Tensor) or not t.is_cuda or not t.is_contiguous():
+                raise LnetoError(f"{what}: {name} must be a contiguous device tensor")
+            if t.dtype not in _dtypes(kind)[0]:
+                raise LnetoError(f"{what}: {name} must be {kind} (got {t.dtype})")
+            if dev is None:
+                dev = t.device
+            elif t.device != dev:
+                raise LnetoError(f"{what}: {name} is on {t.device}, other arguments on {dev}")
+        self.device = dev
+        if stream is not None and stream.device != dev:
+            raise LnetoError(f"{what}: stream is on {stream.device}, tensors on {dev}")
+        self._stream = stream
+        self._ctx = torch.cuda.device(dev)
+
+    def __enter__(self):
+        import torch
+        self._ctx.__enter__()
+        s = self._stream if self._stream is not None else torch.cuda.current_stream(self.device)
+        return s.cuda_stream
+
+    def __exit__(self, *exc):
+        return self._ctx.__exit__(*exc)
+
+
+def _out(what, out, n, dtype, kind, device):
+    """Caller-supplied output: checked like an input and at least n elements; else allocated."""
+    import torch
+    if out is None:
+        return torch.empty(max(n, 0), dtype=dtype, device=device)
+    if not isinstance(out, torch.Tensor) or not out.is_cuda or not out.is_contiguous():
+        raise LnetoError(f"{what}: out must be a contiguous device tensor")
+    if out.dtype not in _dtypes(kind)[0]:
+        raise LnetoError(f"{what}: out must be {kind} (got {out.dtype})")
+    if out.device != device:
+        raise LnetoError(f"{what}: out is on {out.device}, inputs on {device}")
+    if out.numel() < n:
+        raise LnetoError(f"{what}: out holds {out.numel()} elements, {n} needed")
+    return out
+
+
+def _need_len(what, name, t, n):
+    if t is not None and t.numel() < n:
+        raise LnetoError(f"{what}: {name} holds {t.numel()} elements, {n} needed")
 
 
 def crc32_batch(d_bytes, d_off, out=None, stream=None):
@@ -191,26 +251,26 @@ def crc32_batch(d_bytes, d_off, out=None, stream=None):
     Returns an int32 device tensor holding the uint32 CRCs bit-for-bit.
     """
     import torch
-    _dev_check(d_bytes, d_off)
+    what = "lnx_crc32_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
-    if out is None:
-        out = torch.empty(max(n, 0), dtype=torch.int32, device=d_bytes.device)
+    out = _out(what, out, n, torch.int32, "i32", b.device)
     if n > 0:
-        _check(lib.lnx_crc32_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
-                                   _stream_ptr(stream)), "lnx_crc32_batch")
+        with b as s:
+            _check(lib.lnx_crc32_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
     return out
 
 
 def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
     """1 where frame i (payload + trailing LE FCS) passes the FCS check, else 0."""
     import torch
-    _dev_check(d_bytes, d_off)
+    what = "lnx_fcs_verify_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
-    if out is None:
-        out = torch.empty(max(n, 0), dtype=torch.uint8, device=d_bytes.device)
+    out = _out(what, out, n, torch.uint8, "u8", b.device)
     if n > 0:
-        _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
-                                        _stream_ptr(stream)), "lnx_fcs_verify_batch")
+        with b as s:
+            _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
     return out
 
 
@@ -218,13 +278,15 @@ def crc32_segments(d_bytes, d_start, d_len, out=None, stream=None):
     """CRC32 of every frame d_bytes[d_start[i] : d_start[i] + d_len[i]] (lnx_crc32_segments);
     d_start int64, d_len int32; frames in address order, not overlapping."""
     import torch
-    _dev_check(d_bytes, d_start, d_len)
+    what = "lnx_crc32_segments"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_start", d_start, "i64"), ("d_len", d_len, "i32")], stream)
     n = d_start.numel()
-    if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=d_bytes.device)
+    _need_len(what, "d_len", d_len, n)
+    out = _out(what, out, n, torch.int32, "i32", b.device)
     if n > 0:
-        _check(lib.lnx_crc32_segments(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n,
-                                      out.data_ptr(), _stream_ptr(stream)), "lnx_crc32_segments")
+        with b as s:
+            _check(lib.lnx_crc32_segments(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n,
+                                          out.data_ptr(), s), what)
     return out
 
 
@@ -232,13 +294,15 @@ def fcs_append_batch(d_bytes, d_start, d_len, capacity: int, status=None, stream
     """TX FCS append in place (lnx_fcs_append_batch): pad to 60, append LE FCS,
     d_len (int32, updated) += padding + 4.  Returns the uint8 status (0 or 6)."""
     import torch
-    _dev_check(d_bytes, d_start, d_len)
+    what = "lnx_fcs_append_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_start", d_start, "i64"), ("d_len", d_len, "i32")], stream)
     n = d_start.numel()
-    if status is None:
-        status = torch.empty(n, dtype=torch.uint8, device=d_bytes.device)
+    _need_len(what, "d_len", d_len, n)
+    status = _out(what, status, n, torch.uint8, "u8", b.device)
     if n > 0:
-        _check(lib.lnx_fcs_append_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n, capacity,
-                                        status.data_ptr(), _stream_ptr(stream)), "lnx_fcs_append_batch")
+        with b as s:
+            _check(lib.lnx_fcs_append_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n, capacity,
+                                            status.data_ptr(), s), what)
     return status
 
 
@@ -246,14 +310,17 @@ def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
     """ethernet.CRC32Search of every capture d_bytes[d_off[i]:d_off[i+1]] on the GPU
     (lnx_crc32_search_batch).  d_min_off: int64 (N) or None.  Returns int64 (N), -1 = none."""
     import torch
-    _dev_check(d_bytes, d_off, d_min_off)
+    what = "lnx_crc32_search_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64"), ("d_min_off", d_min_off, "i64")],
+               stream)
     n = d_off.numel() - 1
-    if out is None:
-        out = torch.empty(max(n, 0), dtype=torch.int64, device=d_bytes.device)
+    _need_len(what, "d_min_off", d_min_off, n)
+    out = _out(what, out, n, torch.int64, "i64", b.device)
     if n > 0:
-        _check(lib.lnx_crc32_search_batch(d_bytes.data_ptr(), d_off.data_ptr(),
-                                          d_min_off.data_ptr() if d_min_off is not None else None, n,
-                                          out.data_ptr(), _stream_ptr(stream)), "lnx_crc32_search_batch")
+        with b as s:
+            _check(lib.lnx_crc32_search_batch(d_bytes.data_ptr(), d_off.data_ptr(),
+                                              d_min_off.data_ptr() if d_min_off is not None else None, n,
+                                              out.data_ptr(), s), what)
     return out
 
 
@@ -264,13 +331,14 @@ def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None):
     """Receive-path checksum verdict per Ethernet frame (lnx_ingress_verify_batch):
     0 = checks passed / none apply, else lneto's errGeneric code (3 = ErrBadCRC, ...)."""
     import torch
-    _dev_check(d_bytes, d_off)
+    what = "lnx_ingress_verify_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
-    if out is None:
-        out = torch.empty(max(n, 0), dtype=torch.uint8, device=d_bytes.device)
+    out = _out(what, out, n, torch.uint8, "u8", b.device)
     if n > 0:
-        _check(lib.lnx_ingress_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags, out.data_ptr(),
-                                            _stream_ptr(stream)), "lnx_ingress_verify_batch")
+        with b as s:
+            _check(lib.lnx_ingress_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags, out.data_ptr(), s),
+                   what)
     return out
 
 
@@ -280,14 +348,18 @@ def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):
     d_off: int64 (N), d_len: int32 (N), d_seed: int32 (N) or None.  Returns int16 (uint16 bits).
     """
     import torch
-    _dev_check(d_bytes, d_off, d_len, d_seed)
+    what = "lnx_sum16_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64"), ("d_len", d_len, "i32"),
+                      ("d_seed", d_seed, "i32")], stream)
     n = d_off.numel()
-    if out is None:
-        out = torch.empty(n, dtype=torch.int16, device=d_bytes.device)
+    _need_len(what, "d_len", d_len, n)
+    _need_len(what, "d_seed", d_seed, n)
+    out = _out(what, out, n, torch.int16, "i16", b.device)
     if n > 0:
-        _check(lib.lnx_sum16_batch(d_bytes.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
-                                   d_seed.data_ptr() if d_seed is not None else None, n,
-                                   out.data_ptr(), _stream_ptr(stream)), "lnx_sum16_batch")
+        with b as s:
+            _check(lib.lnx_sum16_batch(d_bytes.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                       d_seed.data_ptr() if d_seed is not None else None, n,
+                                       out.data_ptr(), s), what)
     return out
 
 

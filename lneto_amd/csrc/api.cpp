@@ -2,6 +2,7 @@
 // image), argument checks, host-memory and multi-GPU conveniences.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -89,8 +90,8 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 struct DeviceCtx {
-  std::once_flag once;
-  int status = LNX_OK;
+  std::mutex mu;                   // serializes initialization
+  std::atomic<bool> ready{false};  // set once every field below is valid
   void* d_image = nullptr;
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
@@ -122,28 +123,45 @@ const std::vector<uint32_t>& host_image() {
   return img;
 }
 
-// Context of the calling thread's current device (created on first use).
+// Context of the calling thread's current device (created on first use).  A
+// failed initialization (e.g. hipMalloc out of memory) frees what it had
+// allocated and leaves the context uninitialized, so a later call retries.
+int init_ctx(DeviceCtx& c, int dev) {
+  auto fail = [&](hipError_t err, const char* what) {
+    (void)hipFree(c.d_image);
+    (void)hipFree(c.d_search);
+    c.d_image = nullptr;
+    c.d_search = nullptr;
+    return hip_fail(err, what);
+  };
+  hipError_t err = hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (err != hipSuccess) return fail(err, "hipDeviceGetAttribute");
+  const auto& img = host_image();
+  if ((err = hipMalloc(&c.d_image, img.size() * 4)) != hipSuccess) return fail(err, "hipMalloc(image)");
+  if ((err = hipMemcpy(c.d_image, img.data(), img.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(err, "hipMemcpy(image)");
+  const std::vector<uint32_t> st = build_search_tables();
+  if ((err = hipMalloc(reinterpret_cast<void**>(&c.d_search), st.size() * 4)) != hipSuccess)
+    return fail(err, "hipMalloc(search tables)");
+  if ((err = hipMemcpy(c.d_search, st.data(), st.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(err, "hipMemcpy(search tables)");
+  return LNX_OK;
+}
+
 int get_ctx(DeviceCtx** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
   if (dev < 0 || dev >= kMaxDevices) return LNX_ENODEV;
   DeviceCtx& c = g_ctx[dev];
-  std::call_once(c.once, [&] {
-    hipError_t err = hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipDeviceGetAttribute"); return; }
-    const auto& img = host_image();
-    err = hipMalloc(&c.d_image, img.size() * 4);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(image)"); return; }
-    err = hipMemcpy(c.d_image, img.data(), img.size() * 4, hipMemcpyHostToDevice);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(image)"); return; }
-    const std::vector<uint32_t> st = build_search_tables();
-    err = hipMalloc(reinterpret_cast<void**>(&c.d_search), st.size() * 4);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMalloc(search tables)"); return; }
-    err = hipMemcpy(c.d_search, st.data(), st.size() * 4, hipMemcpyHostToDevice);
-    if (err != hipSuccess) { c.status = hip_fail(err, "hipMemcpy(search tables)"); return; }
-  });
-  if (c.status != LNX_OK) return c.status;
+  if (!c.ready.load(std::memory_order_acquire)) {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.ready.load(std::memory_order_relaxed)) {
+      const int st = init_ctx(c, dev);
+      if (st != LNX_OK) return st;
+      c.ready.store(true, std::memory_order_release);
+    }
+  }
   *out = &c;
   return LNX_OK;
 }

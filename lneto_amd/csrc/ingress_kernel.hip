@@ -197,17 +197,17 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
           if (pl + 40 > M) {
             v = kErrInvalidLengthField;
           } else if (proto == 6 || proto == 17) {
-            if (proto == 17 && pl < 8) {
-              v = kErrTruncatedFrame;
-            } else {
-              const uint32_t ul = proto == 17 ? field16(58) : 8u;
-              if (ul < 8) v = kErrInvalidLengthField;
-              else if (ul > pl) v = kErrTruncatedFrame;
-              else {
-                l4_sum = true;
-                pa = 22, pb = 54, la = 54, lb = 54 + pl;  // AddUint32(pl), AddUint32(proto): high halves 0
-                lseed = pl + proto;
-              }
+            // demux6 size-checks the UDP header only; TCP goes straight to the
+            // sum (internet/stack-ip6.go:116-137), whatever pl is.
+            if (proto == 17) {
+              if (pl < 8) v = kErrTruncatedFrame;
+              else if (field16(58) < 8) v = kErrInvalidLengthField;
+              else if (field16(58) > pl) v = kErrTruncatedFrame;
+            }
+            if (v == 0) {
+              l4_sum = true;
+              pa = 22, pb = 54, la = 54, lb = 54 + pl;  // AddUint32(pl), AddUint32(proto): high halves 0
+              lseed = pl + proto;
             }
           }
         }

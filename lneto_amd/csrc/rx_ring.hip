@@ -220,11 +220,14 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
   // Batches go round-robin over the stages; batch k gathers into the slot
   // block of stage k % depth, after that stage's previous batch has drained.
   // The gather (host memcpy, parallel) of batch k+1 overlaps the copies and
-  // kernels of batch k.
-  const uint32_t per = std::max<uint32_t>(1, std::min(r->batch, r->nslots / r->depth));
+  // kernels of batch k.  With fewer slots than stages only nslots stages are
+  // used, so every stage's slot block [sk*per, sk*per + per) lies inside the
+  // pinned pool.
+  const uint32_t depth = std::min(r->depth, r->nslots);
+  const uint32_t per = std::min(r->batch, r->nslots / depth);
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   int rc = LNX_OK;
-  std::vector<std::pair<uint64_t, uint32_t>> pending(r->depth, {0, 0});  // (first frame, count) per stage
+  std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});  // (first frame, count) per stage
   auto drain = [&](uint32_t k) {
     const hipError_t se = hipStreamSynchronize(r->st[k].s);
     if (se != hipSuccess) return hip_error(se, "rx ring hipStreamSynchronize");
@@ -237,7 +240,7 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
   };
   uint64_t i0 = 0;
   for (uint32_t k = 0; i0 < n && rc == LNX_OK; ++k, i0 += per) {
-    const uint32_t sk = k % r->depth;
+    const uint32_t sk = k % depth;
     if (pending[sk].second) rc = drain(sk);
     if (rc != LNX_OK) break;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
@@ -261,7 +264,7 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
     rc = enqueue(r, r->st[sk], s0, nb, offset, flags);
     pending[sk] = {i0, nb};
   }
-  for (uint32_t k = 0; k < r->depth; ++k) {
+  for (uint32_t k = 0; k < depth; ++k) {
     if (!pending[k].second) continue;
     const int d = drain(k);
     if (rc == LNX_OK) rc = d;

@@ -57,6 +57,18 @@ def udp(payload: bytes, length: int | None = None) -> bytes:
     return struct.pack(">HHHH", 5353, 53, ul, 0) + payload
 
 
+def short_tcp6(rng) -> bytes:
+    """0..7 payload bytes under IPv6 next-header TCP; demux6 does no size check
+    for TCP (internet/stack-ip6.go:116-121), so the verdict is the sum alone.
+    Half of the >= 2-byte ones carry their own checksum in the first word."""
+    raw = bytearray(rng.integers(0, 256, size=int(rng.integers(0, 8)), dtype=np.uint8).tobytes())
+    if len(raw) >= 2 and rng.integers(0, 2):
+        hdr = struct.pack(">IHBB", 0x60000000, len(raw), O.IPPROTO_TCP, 64) + bytes(range(0x20, 0x40))
+        raw[0:2] = b"\0\0"
+        raw[0:2] = struct.pack(">H", O.ipv6_pseudo(hdr).payload_sum16(bytes(raw)))
+    return bytes(raw)
+
+
 def frames(seed: int = 1, count: int = 3000) -> list[bytes]:
     """A mixed batch: valid frames of every kind plus every malformation the
     receive path distinguishes, with random payload sizes (odd ones too)."""
@@ -74,6 +86,8 @@ def frames(seed: int = 1, count: int = 3000) -> list[bytes]:
             f = ether(0x0800, ipv4(17, udp(pay())))
         elif kind == 2:  # IP options: the header sum still covers 20 bytes only (ipv4/frame.go:144-146)
             f = ether(0x0800, ipv4(6, tcp(pay()), opts=bytes(4 * int(rng.integers(1, 11)))))
+        elif kind == 3 and (i // 24) % 2:  # IPv6 TCP shorter than a TCP header: demux6 sums it anyway
+            f = ether(0x86DD, ipv6(6, short_tcp6(rng)))
         elif kind == 3:
             f = ether(0x86DD, ipv6(6, tcp(pay())))
         elif kind == 4:

@@ -148,3 +148,19 @@ def test_ring_mtu_batch_roundtrip(cuda):
         assert np.array_equal(np.flatnonzero(ok == 0), bad)
     finally:
         ring.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nslots", [1, 2, 3])
+def test_ingress_packets_fewer_slots_than_stages(cuda, nslots):
+    """A ring with fewer slots than pipeline stages (depth 3) gathers into its
+    own slots only (the stage block used to run past the pool)."""
+    frames = _case_frames(seed=40 + nslots, count=37)
+    ring = L.RxRing(nslots, slot_cap=_cap_for(frames, 0), depth=3)
+    try:
+        ok, verdict = ring.ingress_packets(frames, offset=0)
+    finally:
+        ring.close()
+    want_ok, want_v = _expect(frames)
+    assert np.array_equal(ok, want_ok)
+    assert np.array_equal(verdict, want_v)
