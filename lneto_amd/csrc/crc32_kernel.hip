@@ -287,6 +287,11 @@ __device__ __forceinline__ void ld_run2(uint64_t* o, uint32_t v, __amdgpu_buffer
 #undef LNX_L
 #undef LNX_O
 #undef LNX_I
+// One dwordx2 load with the default cache policy (the line stays in L2).
+template <int IMM>
+__device__ __forceinline__ void ld_x2d(uint64_t& o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx2 %0, %1, %2, 0 offen offset:%3" : "=&v"(o) : "v"(v), "s"(rsrc), "i"(IMM));
+}
 template <int K0, int KS, int D, bool NT>
 __device__ __forceinline__ void ld_item(uint64_t* w, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
   if constexpr (K0 < KS) {
@@ -811,7 +816,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // WL = 1 runs the same slot structure on 32-lane rows (one dword per lane,
 // two frames per wave): lane p is virtual lane p, its register takes F from
 // column (p + a) mod 32, and the row XOR spans the 32 lanes.
-template <CrcMode MODE, int KS, int VAR, int WL = 2, bool JM = true>
+template <CrcMode MODE, int KS, int VAR, int WL = 2, bool JM = true, int EP = 0>
 __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   static_assert(WL == 1 || WL == 2, "words per lane");
   constexpr uint32_t RL = 32 / WL;  // lanes per row
@@ -873,9 +878,33 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   // an out-of-range offset (no memory traffic).  Always issued: an asm load
   // under a branch makes hipcc merge its output with the old value by copies
   // placed before the ring's wait (tools/prof/audit_ring.py caught that).
+  // Cache policy of the step loads (two words per lane).  Consecutive frames
+  // share a line (the one holding the frame boundary), and a wave's four rows
+  // fold four consecutive frames, so most shared lines are asked for twice
+  // within one slot; the first and last chunks' shared lines are asked for by
+  // two different waves.  With non-temporal loads the line is gone from L2 by
+  // the second request and HBM serves it twice.
+  //   EP = 0: every step nt (r1);
+  //   EP = 1: the first step and the last two steps (where a frame's last line
+  //           lies) with the default policy, the middle steps nt (product);
+  //   EP = 2: only the first step with the default policy;
+  //   EP = 3: every step with the default policy.
+  constexpr bool kEdge = (EP == 1 || EP == 2) && WL == 2;
+  constexpr bool kTail = EP == 1 && WL == 2;
+  constexpr bool kAllDef = EP == 3 && WL == 2;
   auto ld_runs = [&]<int K0>(auto self, std::integral_constant<int, K0>, uint32_t voff, uint32_t jmax) {
-    if constexpr (K0 < KS - 1) {
-      constexpr int N = KS - 1 - K0 < 6 ? KS - 1 - K0 : 6;
+    if constexpr (kAllDef && K0 < KS - 1) {
+      if constexpr (WL == 2) ld_x2d<K0 * 128>(w[K0], (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
+      self(self, std::integral_constant<int, K0 + 1>{}, voff, jmax);
+    } else if constexpr (kAllDef) {
+    } else if constexpr (kEdge && K0 == 0) {
+      if constexpr (WL == 2) ld_x2d<0>(w[0], voff, data_rsrc);
+      self(self, std::integral_constant<int, 1>{}, voff, jmax);
+    } else if constexpr (kTail && K0 == KS - 2) {
+      if constexpr (WL == 2) ld_x2d<(KS - 2) * 128>(w[KS - 2], (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
+    } else if constexpr (K0 < KS - 1) {
+      constexpr int KE = kTail ? KS - 2 : KS - 1;  // end of this run of nt loads
+      constexpr int N = KE - K0 < 6 ? KE - K0 : 6;
       if constexpr (WL == 2)
         ld_run2<K0 * 128, N, 128>(w + K0, (uint32_t)K0 < jmax ? voff : kOOB, data_rsrc);
       else
@@ -895,7 +924,9 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       // the last step from its own offset: out of range unless the frame has
       // KS lines (a 1500-B frame spans 12 lines at 29 % of start alignments;
       // the 13th line belongs to the next frame and would be fetched twice)
-      if constexpr (WL == 2)
+      if constexpr (kTail || kAllDef)
+        ld_x2d<(KS - 1) * 128>(w[KS - 1], r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
+      else if constexpr (WL == 2)
         ld_run2<(KS - 1) * 128, 1, 128>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
       else
         ld_run<(KS - 1) * 128, 1, 128, true>(w + KS - 1, r.J >= (uint32_t)KS ? voff : kOOB, data_rsrc);
@@ -1142,7 +1173,7 @@ constexpr uint64_t kLineMean = 4096;
 constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13, int LWL = 2, bool LJM = true>
+          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1280,7 +1311,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     } else if (rl == 16 && lean) {
       // lean rows: 16 lanes x two words (LWL = 2) or 32 lanes x one word (LWL = 1)
       L.p = lane & (32u / LWL - 1u), L.row = lane / (32u / LWL);
-      if constexpr (!SEG) lines_body<MODE, KSL, VAR, LWL, LJM>(lds, L, cx);
+      if constexpr (!SEG) lines_body<MODE, KSL, VAR, LWL, LJM, LEP>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
       rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1>(lds, L, cx);
@@ -1357,6 +1388,12 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       // the product dispatch with the r1 lean rows (junk word reloaded, its U-image taken out), and its loads only
       case 57: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, false); break;
       case 58: LNX_LAUNCH(CrcMode::kCrc, 1, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, false); break;
+      // lean rows by the cache policy of their step loads (lines_body EP): all nt (the r2b product) and
+      // its loads only, the first step at the default policy, every step at the default policy
+      case 90: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 0); break;
+      case 91: LNX_LAUNCH(CrcMode::kCrc, 1, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 0); break;
+      case 92: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 2); break;
+      case 93: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 3); break;
 #undef LNX_LEAN
       // forced 4-lane rows
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;
