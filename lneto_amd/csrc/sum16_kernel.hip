@@ -102,7 +102,13 @@ __device__ __forceinline__ uint64_t keep8(int32_t d) {  // bytes [d, 8) of a qwo
   return (~0ull << q) << q;
 }
 
-template <bool NT, int UNR = kLineUnroll>
+// EDGE (with NT): the first line of each batch and its last two (where a
+// 12- or 13-line segment ends) are loaded with the default cache policy, the
+// rest non-temporally.  Back-to-back segments share a line; a wave's four rows
+// ask for it twice within one batch, and with nt the second request found the
+// line gone from L2 and fetched it from HBM again (the CRC kernel's lean rows
+// showed the same, crc32_kernel.hip lines_body EP).
+template <bool NT, int UNR = kLineUnroll, bool EDGE = true>
 __global__ void __launch_bounds__(kSumBlock)
 sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                    const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed, uint64_t nseg,
@@ -132,8 +138,10 @@ sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     for (uint32_t k0 = 0; k0 < nlw; k0 += UNR) {
       uint64_t x[UNR];
 #pragma unroll
-      for (int u = 0; u < UNR; ++u)
-        x[u] = k0 + u < nl ? (NT ? __builtin_nontemporal_load(base + 16u * (k0 + u)) : base[16u * (k0 + u)]) : 0ull;
+      for (int u = 0; u < UNR; ++u) {
+        const bool nt = NT && !(EDGE && (u == 0 || u >= UNR - 2));
+        x[u] = k0 + u < nl ? (nt ? __builtin_nontemporal_load(base + 16u * (k0 + u)) : base[16u * (k0 + u)]) : 0ull;
+      }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int32_t o0 = (int32_t)(128u * (k0 + u) + 8u * p) - (int32_t)mis;  // segment offset of byte 0
@@ -150,8 +158,9 @@ sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   }
 }
 
-// var 0: line rows (product); var 1: the half-line rows of sum16_segments_kernel; var 2: line rows, default cache
-// policy; var 3 / 4: line rows with 8 / 16 lines in flight
+// var 0: line rows, edge lines at the default policy (product); var 1: the half-line rows of
+// sum16_segments_kernel; var 2: line rows, default cache policy; var 3 / 4: line rows with 8 / 16 lines in
+// flight; var 5: line rows all nt (the r1h product)
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                   const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                   hipStream_t stream, int var) {
@@ -180,6 +189,9 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
   else if (var == 2)
     hipLaunchKernelGGL(sum16_lines_kernel<false>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,
                        len, seed, n, out);
+  else if (var == 5)
+    hipLaunchKernelGGL((sum16_lines_kernel<true, kLineUnroll, false>), dim3((unsigned)grid), dim3(kSumBlock), 0,
+                       stream, bytes, off, len, seed, n, out);
   else
     hipLaunchKernelGGL(sum16_lines_kernel<true>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,
                        len, seed, n, out);

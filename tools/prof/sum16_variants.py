@@ -1,5 +1,7 @@
-"""Time the sum16 kernel variants (0 = line rows nt, 1 = r1c half-line rows, 2 = line rows default policy) on
-1 M x 1500-B segments, round-robin medians.  usage: sum16_variants.py [REPS]"""
+"""Time the sum16 kernel variants (sum16_kernel.hip launch_sum16_segments: 0 = line rows with default-policy
+edge lines, 1 = r1c half-line rows, 2 = line rows default policy, 5 = line rows all nt) on 1 M x 1500-B
+segments, round-robin medians; each variant's sums are checked against variant 1's.
+usage: sum16_variants.py [REPS] [V1,V2,...]"""
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np, torch
@@ -21,9 +23,13 @@ t0 = time.perf_counter()
 while time.perf_counter() - t0 < 0.5:
     launch(0)
 torch.cuda.synchronize()
-res = {0: [], 1: [], 2: [], 3: [], 4: []}
+vs = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 1, 2, 3, 4, 5]
+launch(1)
+ref = out.clone()
+ok = {}
+res = {v: [] for v in vs}
 for r in range(reps):
-    for v in (0, 1, 2, 3, 4):
+    for v in vs:
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         e[0].record(s)
         for _ in range(20):
@@ -31,6 +37,8 @@ for r in range(reps):
         e[1].record(s)
         torch.cuda.synchronize()
         res[v].append(e[0].elapsed_time(e[1]) / 20)
-for v in (0, 1, 2, 3, 4):
+        ok[v] = ok.get(v, True) and torch.equal(out, ref)
+for v in vs:
     ms = float(np.median(res[v]))
-    print(f"sum16 variant {v}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s  [{' '.join(f'{x:.4f}' for x in res[v])}]")
+    tag = "sums ok" if ok[v] else "SUM MISMATCH"
+    print(f"sum16 variant {v}: {ms:.4f} ms  {off[-1] / ms / 1e6:.1f} GB/s  {tag}  [{' '.join(f'{x:.4f}' for x in res[v])}]")
