@@ -401,7 +401,7 @@ struct WaveCtx {
 // carries four frames.  Lane p then holds the registers of "virtual lanes"
 // v = 2p and 2p + 1 of a 32-virtual-lane row; all the window algebra below is
 // in virtual lanes.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG, int WL = 1>
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG, int WL = 1, bool EDGE = true>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t VL = RL * WL;  // virtual lanes per row
@@ -572,7 +572,18 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 #pragma unroll
       for (int k = 0; k < KS; ++k) w[s][k] = (Word)(voff * 0x9E3779B1u + k) * 0x100000001ull;
     } else {
-      ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
+      if constexpr (kLine && WL == 1 && EDGE && KS >= 4) {
+        // whole-line rows: an item's first step (a frame's first line) and
+        // its last two (where a frame's last line lies when its items end on
+        // a full one, e.g. 9000 B) at the default cache policy, so the line two
+        // frames share is fetched once (lines_body EP = 1); the rest nt
+        w[s][0] = ld_buf<0>(voff, data_rsrc);
+        ld_item<1, KS - 2, (int)SB, true>(w[s], voff, data_rsrc);
+        w[s][KS - 2] = ld_buf<(KS - 2) * (int)SB>(voff, data_rsrc);
+        w[s][KS - 1] = ld_buf<(KS - 1) * (int)SB>(voff, data_rsrc);
+      } else {
+        ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
+      }
     }
     jk[s] = ld_buf<0>(jv, data_rsrc);
     // 4. bounds of the next S*NR frames, for this slot's next issue
@@ -1173,7 +1184,7 @@ constexpr uint64_t kLineMean = 4096;
 constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1>
+          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1317,7 +1328,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
       rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1>(lds, L, cx);
     } else if (RLF != 16) {
       L.p = lane & 31u, L.row = lane >> 5;
-      rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG>(lds, L, cx);
+      rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG, 1, REDGE>(lds, L, cx);
     }
   }
   if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
@@ -1394,6 +1405,8 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 91: LNX_LAUNCH(CrcMode::kCrc, 1, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 0); break;
       case 92: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 2); break;
       case 93: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, false, 4, 24, 1, 4, 13, 2, true, 3); break;
+      // the product dispatch with 32-lane line rows all nt (the r1 form)
+      case 97: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, false); break;
 #undef LNX_LEAN
       // forced 4-lane rows
       case 22: LNX_LAUNCH(CrcMode::kCrc, 0, 4); break;
