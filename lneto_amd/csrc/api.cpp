@@ -61,10 +61,11 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
 // byte tables for k = 0..5 (search_kernel.hip).
 // Then the tables of crc32_search_seg_kernel (24-byte lane segments): the
 // byte-step table replicated in 32 bank columns (entry e, column c at 32e + c),
-// Z_{24*2^k} as four byte tables for k = 0..5, and Z_4 as four byte tables.
+// Z_{24*2^k} as four byte tables for k = 0..5, and Z_4 as four byte tables;
+// then Z_{48*2^k} for k = 0..4 (crc32_search_half_kernel, 48-byte segments).
 std::vector<uint32_t> build_search_tables() {
   constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 24;  // = kSearchSeg
-  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024);
+  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
   for (uint32_t k = 0; k < 6; ++k)
     for (uint32_t m = 0; m < 4; ++m)
@@ -77,6 +78,11 @@ std::vector<uint32_t> build_search_tables() {
         t[kOld + 8192 + k * 1024 + m * 256 + e] = zshift_bytes_fast(e << (8 * m), (uint64_t)kSeg << k);
   for (uint32_t m = 0; m < 4; ++m)  // Z_4 (slicing-by-4) for the segment folds
     for (uint32_t e = 0; e < 256; ++e) t[kOld + 8192 + 6 * 1024 + m * 256 + e] = zshift_bytes(e << (8 * m), 4);
+  // crc32_search_half_kernel (48-byte segments): Z_{48*2^k} for k = 0..4
+  for (uint32_t k = 0; k < 5; ++k)
+    for (uint32_t m = 0; m < 4; ++m)
+      for (uint32_t e = 0; e < 256; ++e)
+        t[kOld + 8192 + 7 * 1024 + k * 1024 + m * 256 + e] = zshift_bytes_fast(e << (8 * m), (uint64_t)48 << k);
   return t;
 }
 

@@ -237,11 +237,116 @@ crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __res
   }
 }
 
+
+// Two captures per wave (r2 product): each 32-lane half folds its own capture
+// in blocks of 32 x 48 bytes (1536 bytes: a 1500-B capture is still one block)
+// with the same three phases; the scan spans the half's 32 lanes in five
+// levels of Z_{48*2^k}.  Per byte that is 0.42 scan lookups (shared tables,
+// bank-conflicting) against 1.0 with 24-byte segments over 64 lanes.
+constexpr uint32_t kHalfSeg = 48;
+constexpr uint32_t kHalfTabOff = kSegTabOff + kSegTabDwords;  // Z_{48*2^k}, k = 0..4, in the host tables
+constexpr uint32_t kHalfLdsDwords = 8192 + 5 * 1024 + 1024;    // byte table (32 columns), 5 levels, Z_4
+template <int kZWords>
+__global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
+crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                         int64_t* __restrict__ result) {
+  constexpr uint32_t SEG = kHalfSeg, NW = SEG / 4;
+  __shared__ uint32_t lds[kHalfLdsDwords];
+  for (uint32_t i = threadIdx.x; i < 8192; i += kSegBlock) lds[i] = tables[kSegTabOff + i];
+  for (uint32_t i = threadIdx.x; i < 5 * 1024; i += kSegBlock) lds[8192 + i] = tables[kHalfTabOff + i];
+  for (uint32_t i = threadIdx.x; i < 1024; i += kSegBlock) lds[8192 + 5 * 1024 + i] = tables[kSegTabOff + 8192 + 6 * 1024 + i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, col = lane & 31u, hl = lane & 31u, half = lane >> 5;
+  const uint32_t* bt = lds + col;               // byte table, this lane's column: entry e at bt[32 e]
+  const uint32_t* zt = lds + 8192;              // level k at zt + 1024 k
+  const uint32_t* z4 = lds + 8192 + 5 * 1024;   // Z_4
+  auto bstep = [&](uint32_t r, uint32_t b) -> uint32_t { return bt[((r ^ b) & 0xFFu) << 5] ^ (r >> 8); };
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kSegBlock / 64);
+  for (uint64_t q = (uint64_t)blockIdx.x * (kSegBlock / 64) + (threadIdx.x >> 6); q * 2 < n; q += nwaves) {
+    const uint64_t c = q * 2 + half;
+    const bool live = c < n;
+    const uint64_t s = live ? off[c] : 0, e = live ? off[c + 1] : 0;
+    const int64_t L = e > s ? (int64_t)(e - s) : 0;
+    int64_t m = live && min_off ? min_off[c] : 0;
+    if (m < 0) m = 0;
+    int64_t found = -1;
+    bool act = live && L >= m + 4;  // this half still searching
+    const uint8_t* d = bytes + s;
+    uint32_t carry = 0xFFFFFFFFu;  // register entering the block (CRC init)
+    for (int64_t B = 0; __builtin_amdgcn_ballot_w64(act) != 0; B += 32 * SEG) {
+      const int64_t base = B + (int64_t)(SEG * hl);
+      const uintptr_t a = reinterpret_cast<uintptr_t>(d + base);
+      const uint32_t sh = (uint32_t)(a & 3u);
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
+      const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(d) + (uint64_t)L);  // first byte past the capture
+      const int64_t nd64 = act ? (lim - (int64_t)(a - sh) + 3) >> 2 : 0;
+      const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
+      uint32_t v[NW + 1];
+#pragma unroll
+      for (uint32_t i = 0; i <= NW; ++i) v[i] = (int32_t)i < nd ? wp[i] : 0u;
+      uint32_t u[NW];
+#pragma unroll
+      for (uint32_t i = 0; i < NW; ++i) u[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+      // pass A: the segment's end state from 0 (kZWords words by Z_4, the rest byte by byte)
+      uint32_t l = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < NW; ++i) {
+        if ((int)i < kZWords) {
+          l = zseg(z4, l ^ u[i]);
+        } else {
+#pragma unroll
+          for (uint32_t qq = 0; qq < 4; ++qq) l = bstep(l, u[i] >> (8 * qq));
+        }
+      }
+      if (hl == 0) l ^= zseg(zt, carry);
+      // scan within the half: P holds lanes (hl - 2^k, hl] after step k
+      uint32_t P = l;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t dd = 1u << k;
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)P);
+        P ^= hl >= dd ? zseg(zt + 1024 * k, prev) : 0u;
+      }
+      uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P);
+      r = hl == 0 ? carry : r;
+      // pass B: the register after every byte; the first valid residue per half
+      uint32_t bl0 = 32, bi0 = 0, bl1 = 32, bi1 = 0;  // wave-uniform
+#pragma unroll
+      for (uint32_t i = 0; i < SEG; ++i) {
+        r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
+        if (__builtin_amdgcn_ballot_w64(act && r == kResidueRegister)) {
+          const int64_t k = base + (int64_t)i + 1;
+          const uint64_t ok = __builtin_amdgcn_ballot_w64(act && r == kResidueRegister && k >= m + 4 && k <= L);
+          const uint32_t o0 = (uint32_t)ok, o1 = (uint32_t)(ok >> 32);
+          if (o0) {
+            const uint32_t ln = (uint32_t)__builtin_ctz(o0);
+            if (ln < bl0) bl0 = ln, bi0 = i;
+          }
+          if (o1) {
+            const uint32_t ln = (uint32_t)__builtin_ctz(o1);
+            if (ln < bl1) bl1 = ln, bi1 = i;
+          }
+        }
+      }
+      const uint32_t bl = half ? bl1 : bl0, bi = half ? bi1 : bi0;
+      if (act && bl < 32) found = B + (int64_t)(SEG * bl + bi) + 1 - 4;
+      const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)P, 31);
+      const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+      carry = half ? c1 : c0;
+      act = act && found < 0 && B + (int64_t)(32 * SEG) < L;
+    }
+    if (live && hl == 0) result[c] = found;
+  }
+}
+
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // profiling: LNX_PROF_SEARCH=word selects the word-lane kernel
-  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B, =6 pass A all by Z_4
+  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B, =6 pass A all by Z_4,
+  // =s the 24-byte-segment kernel (one capture per wave, the r1h product);
+  // LNX_PROF_SEARCH_ZWORDS=0|2|4|8|10 the two-capture kernel's pass A split
   static const char mode = [] {
     const char* e = getenv("LNX_PROF_SEARCH");
     return e ? e[0] : '\0';
@@ -262,9 +367,35 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
     else if (mode == '6')  // pass A all Z_4
       hipLaunchKernelGGL((crc32_search_seg_kernel<true, 6>), dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes,
                          off, min_off, n, tables, result);
-    else
+    else if (mode == 's')  // 24-byte segments, one capture per wave (the r1h product)
       hipLaunchKernelGGL((crc32_search_seg_kernel<true, kSearchZWords>), dim3((unsigned)grid), dim3(kSegBlock), 0,
                          stream, bytes, off, min_off, n, tables, result);
+    else {  // two captures per wave, 48-byte segments
+      static const int zw = [] {
+        const char* e = getenv("LNX_PROF_SEARCH_ZWORDS");
+        return e ? atoi(e) : -1;
+      }();
+      uint64_t g2 = ((n + 1) / 2 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+      if (g2 > cap) g2 = cap;
+      if (zw == 0)
+        hipLaunchKernelGGL((crc32_search_half_kernel<0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      else if (zw == 8)
+        hipLaunchKernelGGL((crc32_search_half_kernel<8>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      else if (zw == 2)
+        hipLaunchKernelGGL((crc32_search_half_kernel<2>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      else if (zw == 10)
+        hipLaunchKernelGGL((crc32_search_half_kernel<10>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      else if (zw == 4)
+        hipLaunchKernelGGL((crc32_search_half_kernel<4>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      else  // product: pass A all by Z_4 (r2: 0.707 ms against 0.735 for 8 of 12 words, 0.794 for 2)
+        hipLaunchKernelGGL((crc32_search_half_kernel<12>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+    }
   }
   return hipGetLastError();
 }

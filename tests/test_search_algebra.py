@@ -1,10 +1,13 @@
-"""CPU emulation of crc32_search_seg_kernel's algebra (lneto_amd/csrc/search_kernel.hip).
+"""CPU emulation of the segment-lane CRC32Search kernels' algebra
+(lneto_amd/csrc/search_kernel.hip: crc32_search_seg_kernel, 64 lanes x 24 B,
+six-step scan; crc32_search_half_kernel, the r2 product, 32 lanes x 48 B per
+capture, five-step scan, pass A all through Z_4).
 
-The kernel answers ethernet.CRC32Search (ethernet/crc.go:28-47) for one
-capture per wave, in blocks of 64 lane segments of SEG bytes:
+The kernels answer ethernet.CRC32Search (ethernet/crc.go:28-47) for one
+capture per wave (or half-wave), in blocks of LANES lane segments of SEG bytes:
   pass A  l_j  = segment j folded from register 0 (lane 0 also Z_SEG(carry)),
           its first kSearchZWords words through Z_4, the rest byte by byte,
-  scan    P_j  = XOR_{i<=j} Z_{SEG*(j-i)}(l_i) by six doubling steps with the
+  scan    P_j  = XOR_{i<=j} Z_{SEG*(j-i)}(l_i) by log2(LANES) doubling steps with the
                Z_{SEG*2^k} tables,
   pass B  from P_{j-1} (lane 0: the carry) the register after every byte,
           tested against the residue register 0xDEBB20E3.
@@ -16,13 +19,13 @@ tests/test_search.py checks the kernel itself on the GPU.
 import struct
 
 import numpy as np
+import pytest
 
 from oracle import oracle as O
 
-SEG = 24          # kSearchSeg
-KZ = 2            # kSearchZWords
-LANES = 64
 RESIDUE = 0xDEBB20E3
+# (SEG, LANES, KZ): kSearchSeg / 64 lanes / kSearchZWords, and kHalfSeg / 32 lanes / all 12 words
+SCHEDULES = [(24, 64, 2), (48, 32, 12)]
 
 _T = []
 for _e in range(256):
@@ -50,10 +53,14 @@ def _zshift_table(nbytes):
 
 
 _Z4 = _zshift_table(4)
-_ZLEVEL = [_zshift_table(SEG << k) for k in range(6)]
+_ZLEVELS = {}
 
 
-def seg_search(data: bytes, min_off: int) -> int:
+def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: int = 2) -> int:
+    nlev = LANES.bit_length() - 1
+    if SEG not in _ZLEVELS:
+        _ZLEVELS[SEG] = [_zshift_table(SEG << k) for k in range(6)]
+    _ZLEVEL = _ZLEVELS[SEG]
     L = len(data)
     m = max(min_off, 0)
     if L < m + 4:
@@ -79,7 +86,7 @@ def seg_search(data: bytes, min_off: int) -> int:
             l.append(v)
         # scan: P holds lanes (j - 2^k, j] after step k
         P = list(l)
-        for k in range(6):
+        for k in range(nlev):
             d = 1 << k
             P = [P[j] ^ (_ZLEVEL[k](P[j - d]) if j >= d else 0) for j in range(LANES)]
         # pass B: first valid hit in (lane, byte) order
@@ -95,7 +102,8 @@ def seg_search(data: bytes, min_off: int) -> int:
     return -1
 
 
-def test_seg_schedule_matches_oracle():
+@pytest.mark.parametrize("seg,lanes,kz", SCHEDULES)
+def test_seg_schedule_matches_oracle(seg, lanes, kz):
     rng = np.random.default_rng(31)
     cases = []
     for n in [0, 3, 4, 5, 23, 24, 25, 1499, 1536, 1537, 3100]:
@@ -106,8 +114,8 @@ def test_seg_schedule_matches_oracle():
         cases.append((body + struct.pack("<I", O.crc32(body)) + body[:40], n + 1))
     cases.append((b"\0\0\0\0" + bytes(100), 0))
     # hits straddling lane segments and the 1536-byte block edge
-    for cut in [20, 21, 22, 23, 44, 1532, 1533, 1534, 1535, 1536, 3068]:
+    for cut in [20, 21, 22, 23, 44, 45, 46, 47, 92, 1532, 1533, 1534, 1535, 1536, 3068]:
         body = rng.integers(0, 256, size=cut, dtype=np.uint8).tobytes()
         cases.append((body + struct.pack("<I", O.crc32(body)) + bytes(9), 0))
     for data, mo in cases:
-        assert seg_search(data, mo) == O.crc32_search(data, mo), (len(data), mo)
+        assert seg_search(data, mo, seg, lanes, kz) == O.crc32_search(data, mo), (len(data), mo)
