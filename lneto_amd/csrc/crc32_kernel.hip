@@ -581,6 +581,12 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         ld_item<1, KS - 2, (int)SB, true>(w[s], voff, data_rsrc);
         w[s][KS - 2] = ld_buf<(KS - 2) * (int)SB>(voff, data_rsrc);
         w[s][KS - 1] = ld_buf<(KS - 1) * (int)SB>(voff, data_rsrc);
+      } else if constexpr (kLine && WL == 2 && EDGE && KS >= 4) {
+        // the same for two-word 16-lane rows (dwordx2 per lane, one line per row)
+        ld_x2d<0>(w[s][0], voff, data_rsrc);
+        ld_item<1, KS - 2, (int)SB, true>(w[s], voff, data_rsrc);
+        ld_x2d<(KS - 2) * (int)SB>(w[s][KS - 2], voff, data_rsrc);
+        ld_x2d<(KS - 1) * (int)SB>(w[s][KS - 1], voff, data_rsrc);
       } else {
         ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
       }
@@ -1380,6 +1386,8 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 19: LNX_16(2, 13, 2, 4); break;  // two-slot ring
       case 28: LNX_16(2, 14, 1, 4); break;
       case 29: LNX_16(2, 24, 1, 4); break;  // 24-line items
+      case 43: LNX_16(2, 32, 1, 4); break;  // 32-line items
+      case 44: LNX_16(2, 18, 1, 4); break;
       case 40: LNX_16(2, 13, 1, 8); break;  // 8-frame chunks
       case 41: LNX_16(2, 12, 2, 4); break;
       case 42: LNX_16(2, 13, 1, 16); break;

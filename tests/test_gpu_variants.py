@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 # 50..52: forced lean line rows (lines_body), KSL = 13, 14, 12;
 # 56: the product dispatch with one-word 16-lane rows instead of lean rows;
 # 70: forced lean rows on 32 lanes x one word
-FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97]
+FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97, 43, 44]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
