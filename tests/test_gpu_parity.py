@@ -105,6 +105,29 @@ def test_long_frames(cuda):
     assert list(got) == list(O.crc32_frames(data, off))
 
 
+def test_slice_over_2gib_takes_the_generic_path(cuda):
+    """A workgroup slice of more than 2 GiB does not fit the 31-bit buffer
+    offsets of the pipelined bodies and is folded by rows_generic
+    (crc32_kernel.hip: static per-wave ranges, byte loads): 16 frames of
+    ~136 MB in one slice, the first starting at an odd offset."""
+    import torch
+    lens = np.array([136_000_001 + 17 * i for i in range(16)], dtype=np.int64)
+    off = (synth.offsets_from_lengths(lens) + 5).astype(np.uint64)
+    assert int(off[-1] - off[0]) > (1 << 31)
+    d = synth.bytes_torch(int(off[-1]) + 8, cuda, seed=0x2619)
+    o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+    got = L.crc32_batch(d, o).cpu().numpy().view(np.uint32)
+    host = d.cpu().numpy()
+    want = O.crc32_frames(host, off, threads=8)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0]
+    # FCS verify through the same path: frame 3 gets its LE FCS in its last 4 bytes
+    s3, e3 = int(off[3]), int(off[4])
+    fcs = O.crc32(host[s3:e3 - 4].tobytes())
+    d[e3 - 4:e3] = torch.tensor(list(int(fcs).to_bytes(4, "little")), dtype=torch.uint8, device=cuda)
+    ok = L.fcs_verify_batch(d, o).cpu().numpy()
+    assert list(ok) == [1 if i == 3 else 0 for i in range(16)], list(ok)
+
+
 def test_empty_batch_and_empty_frames(cuda):
     import torch
     d = torch.zeros(16, dtype=torch.uint8, device=cuda)
