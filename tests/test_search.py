@@ -74,3 +74,35 @@ def test_long_captures_many_blocks(cuda):
     want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
     bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
+
+
+def test_two_captures_per_wave_pairs(cuda):
+    """The product kernel folds two captures per wave (crc32_search_half_kernel,
+    one per 32-lane half): pair a long capture (several 1536-byte blocks, hit
+    late or never) with a short or empty one, in both orders, hits on the
+    1536-byte block edges, and an odd capture count (the last wave's second
+    half has no capture)."""
+    rng = np.random.default_rng(23)
+    caps, mins = [], []
+    for i in range(301):
+        long_first = i % 2 == 0
+        n_long = int(rng.integers(3000, 9000))
+        body = rng.integers(0, 256, size=n_long, dtype=np.uint8).tobytes()
+        cut = (int(rng.integers(1, n_long // 1536 + 1)) * 1536 - 4) if i % 3 == 0 else int(rng.integers(0, n_long))
+        long_cap = body[:cut] + struct.pack("<I", O.crc32(body[:cut])) + body[cut:]
+        if i % 5 == 4:
+            long_cap = body  # no hit: every block scanned
+        short = rng.integers(0, 256, size=int(rng.integers(0, 80)), dtype=np.uint8).tobytes()
+        if i % 7 == 0:
+            short = short + struct.pack("<I", O.crc32(short))
+        pair = [long_cap, short] if long_first else [short, long_cap]
+        for c in pair:
+            caps.append(c)
+            mins.append(int(rng.choice([0, 2, len(c) // 3])))
+    caps.append(b"\x01\x02\x03")
+    mins.append(0)
+    assert len(caps) % 2 == 1
+    got = _run(cuda, caps, mins)
+    want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
