@@ -253,6 +253,18 @@ __device__ __forceinline__ void ld_item(uint32_t* w, uint32_t v, __amdgpu_buffer
   }
 }
 
+// The same in runs of R steps whose base is out of range (no memory traffic)
+// unless the item has the run's first step (K0 < ns): an item shorter than KS
+// does not read the bytes past its frame's window (R - 1 junk steps at most).
+template <int K0, int KS, int D, int R>
+__device__ __forceinline__ void ld_item_ns(uint32_t* w, uint32_t v, uint32_t ns, __amdgpu_buffer_rsrc_t rsrc) {
+  if constexpr (K0 < KS) {
+    constexpr int N = KS - K0 < R ? KS - K0 : R;
+    ld_run<K0 * D, N, D, false>(w + K0, (uint32_t)K0 < ns ? v : kOOB, rsrc);
+    ld_item_ns<K0 + N, KS, D, R>(w, v, ns, rsrc);
+  }
+}
+
 // The same with dwordx2 loads (two words per lane; always non-temporal).
 #define LNX_L(k) "buffer_load_dwordx2 %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "] nt\n\t"
 #define LNX_O(k) [o##k] "=&v"(o[k])
@@ -401,7 +413,7 @@ struct WaveCtx {
 // carries four frames.  Lane p then holds the registers of "virtual lanes"
 // v = 2p and 2p + 1 of a 32-virtual-lane row; all the window algebra below is
 // in virtual lanes.
-template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG, int WL = 1, bool EDGE = true>
+template <CrcMode MODE, int RL, int KS, int S, int CH, int VAR, bool SEG, int WL = 1, bool EDGE = true, int NSR = 0>
 __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t VL = RL * WL;  // virtual lanes per row
@@ -587,6 +599,11 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         ld_item<1, KS - 2, (int)SB, true>(w[s], voff, data_rsrc);
         ld_x2d<(KS - 2) * (int)SB>(w[s][KS - 2], voff, data_rsrc);
         ld_x2d<(KS - 1) * (int)SB>(w[s][KS - 1], voff, data_rsrc);
+      } else if constexpr (!kLine && WL == 1 && NSR > 0) {
+        // narrow rows: only the runs the item has (the rest of a short last
+        // item would read the next frames' bytes: 4.82 against 4.56 GB of
+        // HBM traffic on the Zipf mix, profiles/r2zcf_narrow_load_runs.txt)
+        ld_item_ns<0, KS, (int)SB, NSR>(w[s], voff, ns, data_rsrc);
       } else {
         ld_item<0, KS, (int)SB, kLine>(w[s], voff, data_rsrc);
       }
@@ -1190,7 +1207,7 @@ constexpr uint64_t kLineMean = 4096;
 constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true>
+          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1324,14 +1341,14 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
-      rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG>(lds, L, cx);
+      rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG, 1, true, NSR4>(lds, L, cx);
     } else if (rl == 16 && lean) {
       // lean rows: 16 lanes x two words (LWL = 2) or 32 lanes x one word (LWL = 1)
       L.p = lane & (32u / LWL - 1u), L.row = lane / (32u / LWL);
       if constexpr (!SEG) lines_body<MODE, KSL, VAR, LWL, LJM, LEP>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1>(lds, L, cx);
+      rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1, true, MIDW == 2 ? 0 : NSR4>(lds, L, cx);
     } else if (RLF != 16) {
       L.p = lane & 31u, L.row = lane >> 5;
       rows_body<MODE, 32, KSW, SW, CHW, VAR, SEG, 1, REDGE>(lds, L, cx);
@@ -1427,6 +1444,14 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
       case 63: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 16, 2, 4, 32); break;
       case 64: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 12, 2, 4, 64); break;
       case 65: LNX_LAUNCH(CrcMode::kCrc, 0, 4, 24, 1, 16, 2, 4, 64); break;
+      // narrow and one-word 16-lane rows by the runs their item loads (NSR4): 125 every step of
+      // the item (the r2 product: a short last item reads the next frames' bytes), 124 / 120 / 126
+      // runs of 1 / 2 / 6 steps (the product: 4; r2ze/r2zf Zipf 1.057 ms against 1.071 for 2, 1.077
+      // for every step, 1.056 for 6)
+      case 125: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 0); break;
+      case 120: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 2); break;
+      case 124: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 1); break;
+      case 126: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 6); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

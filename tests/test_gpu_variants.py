@@ -25,8 +25,11 @@ pytestmark = pytest.mark.gpu
 # 22..25, 60, 63: forced 4-lane rows (16, 2) with 32-frame chunks, (8, 3), (12, 2), (6, 3), (16, 2) with 16, (16, 2) with 32;
 # 50..52: forced lean line rows (lines_body), KSL = 13, 14, 12;
 # 56: the product dispatch with one-word 16-lane rows instead of lean rows;
-# 70: forced lean rows on 32 lanes x one word
-FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97, 43, 44]
+# 70: forced lean rows on 32 lanes x one word;
+# 125: the product dispatch with 4-lane and one-word 16-lane rows loading every step of an item (r2),
+#   120/124/126: loading runs of 2 / 1 / 6 steps (the product: 4)
+FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97, 43, 44,
+          120, 124, 125, 126]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
