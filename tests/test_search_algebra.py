@@ -25,7 +25,7 @@ from oracle import oracle as O
 
 RESIDUE = 0xDEBB20E3
 # (SEG, LANES, KZ): kSearchSeg / 64 lanes / kSearchZWords, and kHalfSeg / 32 lanes / all 12 words
-SCHEDULES = [(24, 64, 2), (48, 32, 12)]
+SCHEDULES = [(24, 64, 2, False), (48, 32, 12, False), (48, 32, 12, True)]
 
 _T = []
 for _e in range(256):
@@ -56,7 +56,22 @@ _Z4 = _zshift_table(4)
 _ZLEVELS = {}
 
 
-def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: int = 2) -> int:
+# Word-check pass B (r2 product): the register after k = 1..4 bytes of a word
+# is Z_k(r ^ (w & lo_k)) and Z_k is a bijection, so it is the residue register
+# exactly when r ^ (w & lo_k) == Z_{-k}(RESIDUE): four compares against
+# constants per word, then r <- Z_4(r ^ w).
+def _zback(x, nbytes):
+    for _ in range(8 * nbytes):
+        b = x >> 31
+        t = (x ^ 0xEDB88320) if b else x
+        x = ((t << 1) & 0xFFFFFFFF) | b
+    return x
+
+
+RESIDUE_BACK = [None] + [_zback(RESIDUE, k) for k in range(1, 5)]
+
+
+def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: int = 2, WB: bool = False) -> int:
     nlev = LANES.bit_length() - 1
     if SEG not in _ZLEVELS:
         _ZLEVELS[SEG] = [_zshift_table(SEG << k) for k in range(6)]
@@ -93,6 +108,15 @@ def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: in
         for j, seg in enumerate(segs):
             r = carry if j == 0 else P[j - 1]
             base = B + SEG * j
+            if WB:
+                for wi, w in enumerate(struct.unpack("<%dI" % (SEG // 4), seg)):
+                    for kk in range(1, 5):
+                        k = base + 4 * wi + kk
+                        lo = 0xFFFFFFFF >> (32 - 8 * kk)
+                        if r ^ (w & lo) == RESIDUE_BACK[kk] and m + 4 <= k <= L:
+                            return k - 4
+                    r = _Z4(r ^ w)
+                continue
             for i, b in enumerate(seg):
                 r = _byte_step(r, b)
                 k = base + i + 1   # bytes consumed
@@ -102,8 +126,13 @@ def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: in
     return -1
 
 
-@pytest.mark.parametrize("seg,lanes,kz", SCHEDULES)
-def test_seg_schedule_matches_oracle(seg, lanes, kz):
+def test_residue_back_constants():
+    for k in range(1, 5):
+        assert _zshift(RESIDUE_BACK[k], k) == RESIDUE
+
+
+@pytest.mark.parametrize("seg,lanes,kz,wb", SCHEDULES)
+def test_seg_schedule_matches_oracle(seg, lanes, kz, wb):
     rng = np.random.default_rng(31)
     cases = []
     for n in [0, 3, 4, 5, 23, 24, 25, 1499, 1536, 1537, 3100]:
@@ -118,4 +147,4 @@ def test_seg_schedule_matches_oracle(seg, lanes, kz):
         body = rng.integers(0, 256, size=cut, dtype=np.uint8).tobytes()
         cases.append((body + struct.pack("<I", O.crc32(body)) + bytes(9), 0))
     for data, mo in cases:
-        assert seg_search(data, mo, seg, lanes, kz) == O.crc32_search(data, mo), (len(data), mo)
+        assert seg_search(data, mo, seg, lanes, kz, wb) == O.crc32_search(data, mo), (len(data), mo)
