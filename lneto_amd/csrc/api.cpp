@@ -65,7 +65,7 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
 // then Z_{48*2^k} for k = 0..4 (crc32_search_half_kernel, 48-byte segments).
 std::vector<uint32_t> build_search_tables() {
   constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 24;  // = kSearchSeg
-  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024);
+  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024 + 4096);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
   for (uint32_t k = 0; k < 6; ++k)
     for (uint32_t m = 0; m < 4; ++m)
@@ -83,6 +83,11 @@ std::vector<uint32_t> build_search_tables() {
     for (uint32_t m = 0; m < 4; ++m)
       for (uint32_t e = 0; e < 256; ++e)
         t[kOld + 8192 + 7 * 1024 + k * 1024 + m * 256 + e] = zshift_bytes_fast(e << (8 * m), (uint64_t)48 << k);
+  // Z_4 as eight nibble tables, each entry in 32 bank columns: (i, v, c) at (16 i + v) * 32 + c
+  for (uint32_t i = 0; i < 8; ++i)
+    for (uint32_t v = 0; v < 16; ++v)
+      for (uint32_t c = 0; c < 32; ++c)
+        t[kOld + 8192 + 12 * 1024 + (16 * i + v) * 32 + c] = zshift_bytes(v << (4 * i), 4);
   return t;
 }
 
