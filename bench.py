@@ -364,7 +364,7 @@ def main():
             "traffic": None,
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
-                       "search": "lnx::crc32_search_half_kernel<12>"}[args.op],
+                       "search": "lnx::crc32_search_u_kernel<2>"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_launches": len(timed),
             "algorithmic_bytes_per_launch": nbytes,

@@ -65,7 +65,7 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
 // then Z_{48*2^k} for k = 0..4 (crc32_search_half_kernel, 48-byte segments).
 std::vector<uint32_t> build_search_tables() {
   constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 24;  // = kSearchSeg
-  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024 + 4096);
+  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024 + 4096 + 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
   for (uint32_t k = 0; k < 6; ++k)
     for (uint32_t m = 0; m < 4; ++m)
@@ -88,6 +88,9 @@ std::vector<uint32_t> build_search_tables() {
     for (uint32_t v = 0; v < 16; ++v)
       for (uint32_t c = 0; c < 32; ++c)
         t[kOld + 8192 + 12 * 1024 + (16 * i + v) * 32 + c] = zshift_bytes(v << (4 * i), 4);
+  // Z_24 as four byte tables (crc32_search_u_kernel's split chains: half a 48-byte segment)
+  for (uint32_t m = 0; m < 4; ++m)
+    for (uint32_t e = 0; e < 256; ++e) t[kOld + 8192 + 12 * 1024 + 4096 + m * 256 + e] = zshift_bytes(e << (8 * m), 24);
   return t;
 }
 

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include "gf2.hpp"
 
 namespace lnx {
 
@@ -117,6 +118,11 @@ constexpr int kSegBlock = 1024;  // 2 blocks per CU (57 KiB LDS each): 8 waves p
 
 __device__ __forceinline__ uint32_t zseg(const uint32_t* z, uint32_t x) {  // four byte tables at z
   return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
+}
+// zseg(z, x) ^ y with the five-way XOR in two v_bitop3
+__device__ __forceinline__ uint32_t zseg_xor(const uint32_t* z, uint32_t x, uint32_t y) {
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(z[x & 0xFFu], z[256 + ((x >> 8) & 0xFFu)], z[512 + ((x >> 16) & 0xFFu)], 0x96);
+  return __builtin_amdgcn_bitop3_b32(t, z[768 + (x >> 24)], y, 0x96);
 }
 
 // kBallot: pass B tests each byte with one compare into a wave mask and keeps
@@ -246,21 +252,73 @@ crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __res
 constexpr uint32_t kHalfSeg = 48;
 constexpr uint32_t kHalfTabOff = kSegTabOff + kSegTabDwords;  // Z_{48*2^k}, k = 0..4, in the host tables
 constexpr uint32_t kHalfLdsDwords = 8192 + 5 * 1024 + 1024;    // byte table (32 columns), 5 levels, Z_4
-template <int kZWords>
-__global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
-crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
-                         int64_t* __restrict__ result) {
+constexpr uint32_t kHalfNibOff = kHalfTabOff + 5 * 1024;         // Z_4 nibble tables in 32 columns (4096 dwords)
+//
+// Pass B by word checks (WB, the r2 product): the register after k = 1..4
+// bytes of a word entered with register r is Z_k(r ^ (w & lo_k)), lo_k the
+// low k bytes, and Z_k is a bijection of the register, so it equals the
+// residue register exactly when r ^ (w & lo_k) == Z_{-k}(0xDEBB20E3).  A word
+// then costs four compares against constants and one Z_4 step to the next word
+// (kBZ words through the shared Z_4 tables, the rest as four byte steps through
+// the lane's conflict-free column) instead of four dependent byte steps each
+// followed by a compare (tests/test_search_algebra.py restates both).
+constexpr uint32_t kResBack1 = zshift_bytes(kResidueRegister, -1);
+constexpr uint32_t kResBack2 = zshift_bytes(kResidueRegister, -2);
+constexpr uint32_t kResBack3 = zshift_bytes(kResidueRegister, -3);
+constexpr uint32_t kResBack4 = zshift_bytes(kResidueRegister, -4);
+static_assert(kResBack4 == 0xFFFFFFFFu && kResBack1 == 0x00BE26EDu, "residue back-shifts");
+// UL (crc32_search_u_kernel, r2 product): the four Z_4 byte tables in 32
+// lane-private bank columns (the CRC kernel's U layout, 128 KiB), so every Z_4
+// step of pass A and pass B is four conflict-free lookups addressed by v_perm;
+// one 16-wave workgroup per CU.  With pass B by word checks the dependent chain
+// is one Z_4 step per word (four independent lookups), not four byte steps, so
+// four waves per SIMD are enough (r2y: the byte-chain pass B was latency-bound
+// in this layout).
+constexpr uint32_t kULdsDwords = 32768 + 6 * 1024;  // U (Z_4, 32 columns), Z_{48*2^k} for k = 0..4, Z_24
+constexpr uint32_t kZ24Off = kHalfNibOff + 4096;     // Z_24 byte tables in the host tables
+__device__ __forceinline__ uint32_t ulds(const uint32_t* lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+// Z_4(x) ^ y through the U layout: byte k of x is byte 1 of the address (v_perm
+// with the lane's column base), tables m = 1, 3 ride in the +128 immediate
+__device__ __forceinline__ uint32_t ustep_xor(const uint32_t* lds, uint32_t x, uint32_t y, uint32_t b0, uint32_t b1) {
+  const uint32_t a0 = __builtin_amdgcn_perm(x, b0, 0x0c020400u);
+  const uint32_t a1 = __builtin_amdgcn_perm(x, b0, 0x0c020500u);
+  const uint32_t a2 = __builtin_amdgcn_perm(x, b1, 0x0c020600u);
+  const uint32_t a3 = __builtin_amdgcn_perm(x, b1, 0x0c020700u);
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(ulds(lds, a0), ulds(lds, a1 + 128), ulds(lds, a2), 0x96);
+  return __builtin_amdgcn_bitop3_b32(t, ulds(lds, a3 + 128), y, 0x96);
+}
+
+template <int kZWords, bool WB, int kBZ, bool UL>
+__device__ __forceinline__ void search_half_body(uint32_t* lds, const uint8_t* __restrict__ bytes,
+                                                 const uint64_t* __restrict__ off, const int64_t* __restrict__ min_off,
+                                                 uint64_t n, const uint32_t* __restrict__ tables,
+                                                 int64_t* __restrict__ result) {
   constexpr uint32_t SEG = kHalfSeg, NW = SEG / 4;
-  __shared__ uint32_t lds[kHalfLdsDwords];
-  for (uint32_t i = threadIdx.x; i < 8192; i += kSegBlock) lds[i] = tables[kSegTabOff + i];
-  for (uint32_t i = threadIdx.x; i < 5 * 1024; i += kSegBlock) lds[8192 + i] = tables[kHalfTabOff + i];
-  for (uint32_t i = threadIdx.x; i < 1024; i += kSegBlock) lds[8192 + 5 * 1024 + i] = tables[kSegTabOff + 8192 + 6 * 1024 + i];
+  constexpr uint32_t kNib = kBZ < 0 ? 4096u : 0u;  // pass B's Z_4 by lane-private nibble tables
+  constexpr uint32_t kZt = UL ? 32768u : 8192u;     // the scan tables
+  if constexpr (UL) {
+    // thread t expands Z_4 value t (table t >> 8, entry t & 255) into its 32 bank replicas
+    static_assert(kSegBlock == 1024, "one U value per thread");
+    const uint32_t t = threadIdx.x, v = tables[kSegTabOff + 8192 + 6 * 1024 + t];
+    const uint32_t ua = ((t >> 9) << 16) | ((t & 255u) << 8) | (((t >> 8) & 1u) << 7);
+    uint4* row = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + ua);
+    const uint4 v4 = {v, v, v, v};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+  } else {
+    for (uint32_t i = threadIdx.x; i < kNib; i += kSegBlock) lds[kHalfLdsDwords + i] = tables[kHalfNibOff + i];
+    for (uint32_t i = threadIdx.x; i < 8192; i += kSegBlock) lds[i] = tables[kSegTabOff + i];
+    for (uint32_t i = threadIdx.x; i < 1024; i += kSegBlock) lds[8192 + 5 * 1024 + i] = tables[kSegTabOff + 8192 + 6 * 1024 + i];
+  }
+  for (uint32_t i = threadIdx.x; i < 5 * 1024; i += kSegBlock) lds[kZt + i] = tables[kHalfTabOff + i];
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63u, col = lane & 31u, hl = lane & 31u, half = lane >> 5;
   const uint32_t* bt = lds + col;               // byte table, this lane's column: entry e at bt[32 e]
-  const uint32_t* zt = lds + 8192;              // level k at zt + 1024 k
-  const uint32_t* z4 = lds + 8192 + 5 * 1024;   // Z_4
+  const uint32_t* zt = lds + kZt;               // level k at zt + 1024 k
+  const uint32_t* z4 = lds + 8192 + 5 * 1024;   // Z_4 (shared tables; not in the UL layout)
+  const uint32_t ub0 = col << 2, ub1 = ub0 | 65536u;  // UL: the lane's U column bases
   auto bstep = [&](uint32_t r, uint32_t b) -> uint32_t { return bt[((r ^ b) & 0xFFu) << 5] ^ (r >> 8); };
   const uint64_t nwaves = (uint64_t)gridDim.x * (kSegBlock / 64);
   for (uint64_t q = (uint64_t)blockIdx.x * (kSegBlock / 64) + (threadIdx.x >> 6); q * 2 < n; q += nwaves) {
@@ -290,8 +348,19 @@ crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __re
       for (uint32_t i = 0; i < NW; ++i) u[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
       // pass A: the segment's end state from 0 (kZWords words by Z_4, the rest byte by byte)
       uint32_t l = 0;
+      if constexpr (UL) {
+        uint32_t x = u[0];
 #pragma unroll
-      for (uint32_t i = 0; i < NW; ++i) {
+        for (uint32_t i = 0; i + 1 < NW; ++i) x = ustep_xor(lds, x, u[i + 1], ub0, ub1);
+        l = ustep_xor(lds, x, 0u, ub0, ub1);
+      } else if constexpr (kZWords == (int)NW && WB) {  // every word by Z_4: the next word rides in the second v_bitop3
+        uint32_t x = u[0];
+#pragma unroll
+        for (uint32_t i = 0; i + 1 < NW; ++i) x = zseg_xor(z4, x, u[i + 1]);
+        l = zseg_xor(z4, x, 0u);
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < ((kZWords == (int)NW && WB) || UL ? 0u : NW); ++i) {
         if ((int)i < kZWords) {
           l = zseg(z4, l ^ u[i]);
         } else {
@@ -306,14 +375,70 @@ crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __re
       for (int k = 0; k < 5; ++k) {
         const uint32_t dd = 1u << k;
         const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)P);
-        P ^= hl >= dd ? zseg(zt + 1024 * k, prev) : 0u;
+        if constexpr (WB) {
+          if (hl >= dd) P = zseg_xor(zt + 1024 * k, prev, P);
+        } else {
+          P ^= hl >= dd ? zseg(zt + 1024 * k, prev) : 0u;
+        }
       }
       uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P);
       r = hl == 0 ? carry : r;
       // pass B: the register after every byte; the first valid residue per half
       uint32_t bl0 = 32, bi0 = 0, bl1 = 32, bi1 = 0;  // wave-uniform
+      if constexpr (WB) {
+        // byte index bi of the segment is a valid candidate when base + bi + 1 is in [m + 4, L]
+        const int64_t lo64 = m + 3 - base, hi64 = L - 1 - base;
+        const int32_t vlo = lo64 < 0 ? 0 : (lo64 > 64 ? 64 : (int32_t)lo64);
+        const int32_t vhi = hi64 < 0 ? -1 : (hi64 > 64 ? 64 : (int32_t)hi64);
+        const uint64_t actm = __builtin_amdgcn_ballot_w64(act);
 #pragma unroll
-      for (uint32_t i = 0; i < SEG; ++i) {
+        for (uint32_t i = 0; i < NW; ++i) {
+          const uint32_t w = u[i];
+          const bool h1 = (r ^ (w & 0xFFu)) == kResBack1, h2 = (r ^ (w & 0xFFFFu)) == kResBack2;
+          const bool h3 = (r ^ (w & 0xFFFFFFu)) == kResBack3;
+          uint32_t x = r ^ w;
+          const bool h4 = x == kResBack4;
+          const uint64_t any = (__builtin_amdgcn_ballot_w64(h1) | __builtin_amdgcn_ballot_w64(h2) |
+                                __builtin_amdgcn_ballot_w64(h3) | __builtin_amdgcn_ballot_w64(h4)) & actm;
+          if (any) {
+            const bool hk[4] = {h1, h2, h3, h4};
+#pragma unroll
+            for (uint32_t kk = 0; kk < 4; ++kk) {
+              const int32_t bi = (int32_t)(4 * i + kk);
+              const uint64_t ok = __builtin_amdgcn_ballot_w64(hk[kk] && bi >= vlo && bi <= vhi) & actm;
+              const uint32_t o0 = (uint32_t)ok, o1 = (uint32_t)(ok >> 32);
+              if (o0) {
+                const uint32_t ln = (uint32_t)__builtin_ctz(o0);
+                if (ln < bl0) bl0 = ln, bi0 = 4 * i + kk;
+              }
+              if (o1) {
+                const uint32_t ln = (uint32_t)__builtin_ctz(o1);
+                if (ln < bl1) bl1 = ln, bi1 = 4 * i + kk;
+              }
+            }
+          }
+          if (i + 1 < NW) {
+            if constexpr (UL) {
+              r = ustep_xor(lds, x, 0u, ub0, ub1);
+            } else if constexpr (kBZ < 0) {
+              const uint32_t* nb = lds + kHalfLdsDwords + col;  // (i, v) at nb[32 (16 i + v)]
+              uint32_t y[8];
+#pragma unroll
+              for (uint32_t q = 0; q < 8; ++q) y[q] = nb[(16u * q + ((x >> (4 * q)) & 15u)) << 5];
+              r = (y[0] ^ y[1] ^ y[2]) ^ (y[3] ^ y[4] ^ y[5]) ^ (y[6] ^ y[7]);
+            } else if ((int)i < kBZ) {
+              r = zseg(z4, x);
+            } else {
+              // Z_4(x) as four byte steps on the pre-XOR-ed word (conflict-free column)
+#pragma unroll
+              for (uint32_t qq = 0; qq < 4; ++qq) x = bt[(x & 0xFFu) << 5] ^ (x >> 8);
+              r = x;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < (WB ? 0u : SEG); ++i) {
         r = bstep(r, u[i >> 2] >> (8 * (i & 3)));
         if (__builtin_amdgcn_ballot_w64(act && r == kResidueRegister)) {
           const int64_t k = base + (int64_t)i + 1;
@@ -338,6 +463,236 @@ crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __re
     }
     if (live && hl == 0) result[c] = found;
   }
+}
+
+template <int kZWords, bool WB = false, int kBZ = 12>
+__global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
+crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                         const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                         int64_t* __restrict__ result) {
+  __shared__ uint32_t lds[kHalfLdsDwords + (kBZ < 0 ? 4096u : 0u)];
+  search_half_body<kZWords, WB, kBZ, false>(lds, bytes, off, min_off, n, tables, result);
+}
+
+// The UL product body: NC captures per half-wave folded side by side, so each
+// lane carries NC independent Z_4 chains through pass A and pass B (one 16-wave
+// block per CU leaves four waves per SIMD to hide the LDS latency; r2s2e: one
+// capture per half ran 0.666 ms against 0.624 for the two-block form).
+template <int NC, bool SPLIT = false>
+__device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __restrict__ bytes,
+                                              const uint64_t* __restrict__ off, const int64_t* __restrict__ min_off,
+                                              uint64_t n, const uint32_t* __restrict__ tables,
+                                              int64_t* __restrict__ result) {
+  constexpr uint32_t SEG = kHalfSeg, NW = SEG / 4;
+  {
+    static_assert(kSegBlock == 1024, "one U value per thread");
+    const uint32_t t = threadIdx.x, v = tables[kSegTabOff + 8192 + 6 * 1024 + t];
+    const uint32_t ua = ((t >> 9) << 16) | ((t & 255u) << 8) | (((t >> 8) & 1u) << 7);
+    uint4* row = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + ua);
+    const uint4 v4 = {v, v, v, v};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+  }
+  for (uint32_t i = threadIdx.x; i < 5 * 1024; i += kSegBlock) lds[32768 + i] = tables[kHalfTabOff + i];
+  if constexpr (SPLIT) lds[32768 + 5 * 1024 + threadIdx.x] = tables[kZ24Off + threadIdx.x];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, col = lane & 31u, hl = lane & 31u, half = lane >> 5;
+  const uint32_t* zt = lds + 32768;  // Z_{48*2^k} at zt + 1024 k (shared)
+  const uint32_t* z24 = lds + 32768 + 5 * 1024;  // SPLIT: Z_24 (shared)
+  const uint32_t ub0 = col << 2, ub1 = ub0 | 65536u;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kSegBlock / 64);
+  constexpr uint64_t CPW = 2 * NC;  // captures per wave: capture 2j + half of the group in half `half`
+  struct Grp {
+    uint64_t s[NC], e[NC];
+    int64_t m[NC];
+  };
+  auto load_grp = [&](uint64_t qq, Grp& g) {
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const uint64_t cc = qq * CPW + 2 * j + half;
+      const bool lv = cc < n;
+      g.s[j] = lv ? off[cc] : 0;
+      g.e[j] = lv ? off[cc + 1] : 0;
+      g.m[j] = lv && min_off ? min_off[cc] : 0;
+    }
+  };
+  // the words of block B of each capture of a group (only dwords holding a capture byte)
+  auto load_words = [&](const Grp& g, int64_t B, const bool (&ac)[NC], uint32_t (&v)[NC][NW + 1]) {
+    const int64_t base = B + (int64_t)(SEG * hl);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const uint8_t* dj = bytes + g.s[j];
+      const int64_t Lj = g.e[j] > g.s[j] ? (int64_t)(g.e[j] - g.s[j]) : 0;
+      const uintptr_t a = reinterpret_cast<uintptr_t>(dj + base);
+      const uint32_t sh = (uint32_t)(a & 3u);
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
+      const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(dj) + (uint64_t)Lj);
+      const int64_t nd64 = ac[j] ? (lim - (int64_t)(a - sh) + 3) >> 2 : 0;
+      const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
+#pragma unroll
+      for (uint32_t i = 0; i <= NW; ++i) v[j][i] = (int32_t)i < nd ? wp[i] : 0u;
+    }
+  };
+  const uint64_t q0 = (uint64_t)blockIdx.x * (kSegBlock / 64) + (threadIdx.x >> 6);
+  for (uint64_t q = q0; q * CPW < n; q += nwaves) {
+    uint64_t c[NC];
+    bool live[NC], act[NC];
+    int64_t L[NC], m[NC], found[NC];
+    const uint8_t* d[NC];
+    uint32_t carry[NC];
+    Grp gc;
+    load_grp(q, gc);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      c[j] = q * CPW + 2 * j + half;
+      live[j] = c[j] < n;
+      const uint64_t s_ = gc.s[j], e_ = gc.e[j];
+      L[j] = e_ > s_ ? (int64_t)(e_ - s_) : 0;
+      m[j] = gc.m[j];
+      if (m[j] < 0) m[j] = 0;
+      found[j] = -1;
+      act[j] = live[j] && L[j] >= m[j] + 4;
+      d[j] = bytes + s_;
+      carry[j] = 0xFFFFFFFFu;
+    }
+    auto any_act = [&]() {
+      bool a = false;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) a = a || act[j];
+      return __builtin_amdgcn_ballot_w64(a) != 0;
+    };
+    for (int64_t B = 0; any_act(); B += 32 * SEG) {
+      const int64_t base = B + (int64_t)(SEG * hl);
+      uint32_t u[NC][NW];
+      {
+        uint32_t v[NC][NW + 1];
+        load_words(gc, B, act, v);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(d[j]) + (uint64_t)base) & 3u);
+#pragma unroll
+          for (uint32_t i = 0; i < NW; ++i) u[j][i] = __builtin_amdgcn_alignbyte(v[j][i + 1], v[j][i], sh);
+        }
+      }
+      // pass A: each segment's end state from 0, the NC chains side by side.
+      // SPLIT: each segment as two independent 24-byte chains, joined by Z_24
+      // (la: words 0..5, kept for pass B's second chain)
+      constexpr uint32_t NH = SPLIT ? NW / 2 : NW;
+      uint32_t x[NC], xb[NC], la[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) x[j] = u[j][0], xb[j] = u[j][NH % NW];
+#pragma unroll
+      for (uint32_t i = 0; i + 1 < NH; ++i)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          x[j] = ustep_xor(lds, x[j], u[j][i + 1], ub0, ub1);
+          if constexpr (SPLIT) xb[j] = ustep_xor(lds, xb[j], u[j][NH + i + 1], ub0, ub1);
+        }
+      uint32_t P[NC];
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        if constexpr (SPLIT) {
+          la[j] = ustep_xor(lds, x[j], 0u, ub0, ub1);
+          P[j] = zseg_xor(z24, la[j], ustep_xor(lds, xb[j], 0u, ub0, ub1));
+        } else {
+          P[j] = ustep_xor(lds, x[j], 0u, ub0, ub1);
+        }
+        if (hl == 0) P[j] ^= zseg(zt, carry[j]);
+      }
+      // scan within the half
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const uint32_t dd = 1u << k;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)P[j]);
+          if (hl >= dd) P[j] = zseg_xor(zt + 1024 * k, prev, P[j]);
+        }
+      }
+      uint32_t r[NC], rb[NC];
+      int32_t vlo[NC], vhi[NC];
+      uint64_t actm[NC];
+      uint32_t bl0[NC], bi0[NC], bl1[NC], bi1[NC];  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P[j]);
+        r[j] = hl == 0 ? carry[j] : pr;
+        if constexpr (SPLIT) rb[j] = zseg_xor(z24, r[j], la[j]);  // the register entering word NH
+        const int64_t lo64 = m[j] + 3 - base, hi64 = L[j] - 1 - base;
+        vlo[j] = lo64 < 0 ? 0 : (lo64 > 64 ? 64 : (int32_t)lo64);
+        vhi[j] = hi64 < 0 ? -1 : (hi64 > 64 ? 64 : (int32_t)hi64);
+        actm[j] = __builtin_amdgcn_ballot_w64(act[j]);
+        bl0[j] = 32, bi0[j] = 0, bl1[j] = 32, bi1[j] = 0;
+      }
+      // pass B by word checks (see crc32_search_half_kernel), the chains side by side
+      // (SPLIT: word i of the first half and word NH + i of the second together)
+      constexpr int NCH = SPLIT ? 2 : 1;
+#pragma unroll
+      for (uint32_t ii = 0; ii < NH; ++ii) {
+#pragma unroll
+        for (int jh = 0; jh < NC * NCH; ++jh) {
+          const int j = jh % NC, h = jh / NC;
+          const uint32_t i = ii + (uint32_t)h * NH;
+          const uint32_t w = u[j][i], rr = h ? rb[j] : r[j];
+          const bool h1 = (rr ^ (w & 0xFFu)) == kResBack1, h2 = (rr ^ (w & 0xFFFFu)) == kResBack2;
+          const bool h3 = (rr ^ (w & 0xFFFFFFu)) == kResBack3;
+          const uint32_t xx = rr ^ w;
+          const bool h4 = xx == kResBack4;
+          const uint64_t any = (__builtin_amdgcn_ballot_w64(h1) | __builtin_amdgcn_ballot_w64(h2) |
+                                __builtin_amdgcn_ballot_w64(h3) | __builtin_amdgcn_ballot_w64(h4)) & actm[j];
+          if (any) {
+            const bool hk[4] = {h1, h2, h3, h4};
+#pragma unroll
+            for (uint32_t kk = 0; kk < 4; ++kk) {
+              const int32_t bi = (int32_t)(4 * i + kk);
+              const uint64_t ok = __builtin_amdgcn_ballot_w64(hk[kk] && bi >= vlo[j] && bi <= vhi[j]) & actm[j];
+              const uint32_t o0 = (uint32_t)ok, o1 = (uint32_t)(ok >> 32);
+              // hits arrive in byte order within a chain; with two chains a lane's
+              // later-half hit can come first, so ties keep the smaller byte
+              if (o0) {
+                const uint32_t ln = (uint32_t)__builtin_ctz(o0);
+                if (ln < bl0[j] || (SPLIT && ln == bl0[j] && 4 * i + kk < bi0[j])) bl0[j] = ln, bi0[j] = 4 * i + kk;
+              }
+              if (o1) {
+                const uint32_t ln = (uint32_t)__builtin_ctz(o1);
+                if (ln < bl1[j] || (SPLIT && ln == bl1[j] && 4 * i + kk < bi1[j])) bl1[j] = ln, bi1[j] = 4 * i + kk;
+              }
+            }
+          }
+          if (ii + 1 < NH) {
+            if (h)
+              rb[j] = ustep_xor(lds, xx, 0u, ub0, ub1);
+            else
+              r[j] = ustep_xor(lds, xx, 0u, ub0, ub1);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const uint32_t bl = half ? bl1[j] : bl0[j], bi = half ? bi1[j] : bi0[j];
+        if (act[j] && bl < 32) found[j] = B + (int64_t)(SEG * bl + bi) + 1 - 4;
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)P[j], 31);
+        const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)P[j], 63);
+        carry[j] = half ? c1 : c0;
+        act[j] = act[j] && found[j] < 0 && B + (int64_t)(32 * SEG) < L[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (live[j] && hl == 0) result[c[j]] = found[j];
+  }
+}
+
+template <int NC, bool SPLIT = false>
+__global__ void __launch_bounds__(kSegBlock, 1)
+crc32_search_u_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                      const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                      int64_t* __restrict__ result) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kULdsDwords];
+  if constexpr (NC == 0)
+    search_half_body<12, true, 0, true>(lds, bytes, off, min_off, n, tables, result);
+  else
+    search_u_body<NC, SPLIT>(lds, bytes, off, min_off, n, tables, result);
 }
 
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
@@ -377,24 +732,77 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
       }();
       uint64_t g2 = ((n + 1) / 2 + kSegBlock / 64 - 1) / (kSegBlock / 64);
       if (g2 > cap) g2 = cap;
-      if (zw == 0)
+      if (mode != '0' && zw == 0)
         hipLaunchKernelGGL((crc32_search_half_kernel<0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      else if (zw == 8)
+      else if (mode != '0' && zw == 8)
         hipLaunchKernelGGL((crc32_search_half_kernel<8>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      else if (zw == 2)
+      else if (mode != '0' && zw == 2)
         hipLaunchKernelGGL((crc32_search_half_kernel<2>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      else if (zw == 10)
+      else if (mode != '0' && zw == 10)
         hipLaunchKernelGGL((crc32_search_half_kernel<10>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      else if (zw == 4)
+      else if (mode != '0' && zw == 4)
         hipLaunchKernelGGL((crc32_search_half_kernel<4>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      else  // product: pass A all by Z_4 (r2: 0.707 ms against 0.735 for 8 of 12 words, 0.794 for 2)
+      else if (mode == 'b')  // r2 byte-chain pass B (pass A all by Z_4)
         hipLaunchKernelGGL((crc32_search_half_kernel<12>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
+      else if (mode == '0' && zw == 8)  // word checks with byte-chain steps, pass A 8 of 12 words by Z_4
+        hipLaunchKernelGGL((crc32_search_half_kernel<8, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '0' && zw == 6)
+        hipLaunchKernelGGL((crc32_search_half_kernel<6, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '0' && zw == 4)
+        hipLaunchKernelGGL((crc32_search_half_kernel<4, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '0' && zw == 10)
+        hipLaunchKernelGGL((crc32_search_half_kernel<10, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '0')  // word checks, pass B's Z_4 steps all as byte chains
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == 'n')  // word checks, pass B's Z_4 steps by lane-private nibble tables
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, -1>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '2')  // word checks, 2 of 11 pass-B steps by Z_4
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 2>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '4')  // word checks, 4 of 11 pass-B steps by the shared Z_4 tables
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 4>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == '8')  // word checks, 8 of 11 by Z_4
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 8>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == 'z')  // word checks, every pass-B step by the shared Z_4 tables (bank conflicts)
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 12>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == 'x')  // word checks with byte-chain Z_4 steps, shared Z_4 in pass A, 2 blocks per CU (r2s2d)
+        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
+                           bytes, off, min_off, n, tables, result);
+      else if (mode == 'u') {  // the U layout with one capture per half (r2s2e)
+        const uint64_t g1 = g2 < (uint64_t)num_cus ? g2 : (uint64_t)num_cus;
+        hipLaunchKernelGGL(crc32_search_u_kernel<0>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
+                           min_off, n, tables, result);
+      } else if (mode == '1') {  // U layout, one capture per half, each segment as two 24-byte chains
+        const uint64_t g1 = g2 < (uint64_t)num_cus ? g2 : (uint64_t)num_cus;
+        hipLaunchKernelGGL((crc32_search_u_kernel<1, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      } else if (mode == 'q') {  // U layout, two captures per half, each segment as two 24-byte chains
+        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
+        hipLaunchKernelGGL((crc32_search_u_kernel<2, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
+                           off, min_off, n, tables, result);
+      } else {  // product: word checks, every Z_4 step through the lane-private U layout, one block per CU,
+                // two captures per half-wave (r2s2f; prefetching the next group's words measured slower, r2s2g)
+        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
+        hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
+                           min_off, n, tables, result);
+      }
     }
   }
   return hipGetLastError();

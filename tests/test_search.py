@@ -77,8 +77,8 @@ def test_long_captures_many_blocks(cuda):
 
 
 def test_two_captures_per_wave_pairs(cuda):
-    """The product kernel folds two captures per wave (crc32_search_half_kernel,
-    one per 32-lane half): pair a long capture (several 1536-byte blocks, hit
+    """Captures share a wave (the r2 kernels fold one or two per 32-lane half,
+    crc32_search_u_kernel<2> four per wave): pair a long capture (several 1536-byte blocks, hit
     late or never) with a short or empty one, in both orders, hits on the
     1536-byte block edges, and an odd capture count (the last wave's second
     half has no capture)."""
@@ -106,3 +106,24 @@ def test_two_captures_per_wave_pairs(cuda):
     want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
     bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
     assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 5, 6, 7, 257])
+def test_four_captures_per_wave_groups(cuda, count):
+    """crc32_search_u_kernel<2> folds captures 4q .. 4q + 3 in one wave (two
+    per 32-lane half, side by side): every group size at the end of the batch,
+    and groups whose four captures end in different 1536-byte blocks (the
+    block loop runs until the last of them is done)."""
+    rng = np.random.default_rng(100 + count)
+    caps, mins = [], []
+    for i in range(count):
+        n_body = int(rng.choice([0, 3, 40, 1500, 1536, 3000, 4700]))
+        body = rng.integers(0, 256, size=n_body, dtype=np.uint8).tobytes()
+        if i % 3 != 2:
+            cut = int(rng.integers(0, n_body + 1))
+            body = body[:cut] + struct.pack("<I", O.crc32(body[:cut])) + body[cut:]
+        caps.append(body)
+        mins.append(int(rng.choice([0, 1, len(body) // 2])))
+    got = _run(cuda, caps, mins)
+    want = [O.crc32_search(c, m) for c, m in zip(caps, mins)]
+    assert list(got) == want

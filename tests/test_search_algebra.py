@@ -1,7 +1,8 @@
 """CPU emulation of the segment-lane CRC32Search kernels' algebra
 (lneto_amd/csrc/search_kernel.hip: crc32_search_seg_kernel, 64 lanes x 24 B,
-six-step scan; crc32_search_half_kernel, the r2 product, 32 lanes x 48 B per
-capture, five-step scan, pass A all through Z_4).
+six-step scan; crc32_search_half_kernel / crc32_search_u_kernel, 32 lanes x 48 B
+per capture, five-step scan, pass A all through Z_4, and the r2 product's pass B
+by word checks, WB).
 
 The kernels answer ethernet.CRC32Search (ethernet/crc.go:28-47) for one
 capture per wave (or half-wave), in blocks of LANES lane segments of SEG bytes:
@@ -124,6 +125,31 @@ def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: in
                     return k - 4
         carry = P[LANES - 1]
     return -1
+
+
+def test_split_chain_identity():
+    """crc32_search_u_kernel<NC, SPLIT>: a 48-byte segment folded as two
+    24-byte chains joins as Z_24(la) ^ lb, and pass B's second chain starts from
+    Z_24(r0) ^ la (la, lb: the halves folded from register 0)."""
+    rng = np.random.default_rng(5)
+    z24 = _zshift_table(24)
+    for _ in range(200):
+        seg = rng.integers(0, 256, size=48, dtype=np.uint8).tobytes()
+        w = struct.unpack("<12I", seg)
+        r0 = int(rng.integers(0, 1 << 32))
+        la = lb = 0
+        for x in w[:6]:
+            la = _Z4(la ^ x)
+        for x in w[6:]:
+            lb = _Z4(lb ^ x)
+        full = 0
+        for x in w:
+            full = _Z4(full ^ x)
+        assert z24(la) ^ lb == full
+        r = r0
+        for x in w[:6]:
+            r = _Z4(r ^ x)
+        assert z24(r0) ^ la == r
 
 
 def test_residue_back_constants():
