@@ -529,6 +529,7 @@ __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __re
       const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(dj) + (uint64_t)Lj);
       const int64_t nd64 = ac[j] ? (lim - (int64_t)(a - sh) + 3) >> 2 : 0;
       const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
+      // one dword per lane per load (16-byte loads measured slower, r2s2i)
 #pragma unroll
       for (uint32_t i = 0; i <= NW; ++i) v[j][i] = (int32_t)i < nd ? wp[i] : 0u;
     }
