@@ -231,6 +231,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       // header sum takes nothing.
       const int32_t qend = (kend + 1) >> 1;
       bool first = true;
+      uint2 yl = make_uint2(0u, 0u);  // the row's last qword, on the lane that loaded it (outside the first qwords)
       for (int32_t q0 = qstart + (int32_t)p; q0 < qend; q0 += 16 * UNR) {
         if (!first) {
 #pragma unroll
@@ -253,14 +254,28 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
               tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
             } else {
-              const uint32_t xt = w & ~ing_keep_from(lb - o0);
-              tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
-              tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
+              // summed whole: only the row's last loaded qword (qend - 1) can
+              // hold bytes at or past lb (every earlier one ends at or before
+              // it); the lane holding it keeps it and takes those bytes back
+              // out after the loop
+              tE = __builtin_amdgcn_udot4(w, wE, tE, false);
+              tO = __builtin_amdgcn_udot4(w, wO, tO, false);
             }
           }
         }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const bool isl = q0 + 16 * u == qend - 1 && !(u == 0 && first);
+          yl.x = isl ? y[u].x : yl.x;
+          yl.y = isl ? y[u].y : yl.y;
+        }
         first = false;
       }
+      // bytes at or past lb of the last qword (zero unless this lane kept it)
+      const int32_t ol = 8 * (qend - 1) - (int32_t)mis;  // frame offset of its first byte
+      const uint32_t j0 = yl.x & ing_keep_from(lb - ol), j1 = yl.y & ing_keep_from(lb - ol - 4);
+      tE -= __builtin_amdgcn_udot4(j0, wE, __builtin_amdgcn_udot4(j1, wE, 0u, false), false);
+      tO -= __builtin_amdgcn_udot4(j0, wO, __builtin_amdgcn_udot4(j1, wO, 0u, false), false);
     }
     for (int32_t k0 = kstart + (int32_t)p; !QW && k0 < kend; k0 += 16 * UNR) {
       if (k0 != kstart + (int32_t)p) {
