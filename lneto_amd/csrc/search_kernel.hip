@@ -336,7 +336,7 @@ __device__ __forceinline__ void search_half_body(uint32_t* lds, const uint8_t* _
       const int64_t base = B + (int64_t)(SEG * hl);
       const uintptr_t a = reinterpret_cast<uintptr_t>(d + base);
       const uint32_t sh = (uint32_t)(a & 3u);
-      const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(d + base - sh);  // global, not flat (see search_u_body)
       const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(d) + (uint64_t)L);  // first byte past the capture
       const int64_t nd64 = act ? (lim - (int64_t)(a - sh) + 3) >> 2 : 0;
       const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
@@ -525,7 +525,10 @@ __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __re
       const int64_t Lj = g.e[j] > g.s[j] ? (int64_t)(g.e[j] - g.s[j]) : 0;
       const uintptr_t a = reinterpret_cast<uintptr_t>(dj + base);
       const uint32_t sh = (uint32_t)(a & 3u);
-      const uint32_t* wp = reinterpret_cast<const uint32_t*>(a - sh);
+      // pointer arithmetic on the kernel argument (not an integer cast), so the
+      // loads are global_load (vmcnt only): flat loads also count in lgkmcnt,
+      // and every wait for an LDS lookup would then wait for them too
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(dj + base - sh);
       const int64_t lim = (int64_t)(reinterpret_cast<uintptr_t>(dj) + (uint64_t)Lj);
       const int64_t nd64 = ac[j] ? (lim - (int64_t)(a - sh) + 3) >> 2 : 0;
       const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
