@@ -7,7 +7,8 @@ lnx_crc32_batch call over the rank's whole frame batch (inputs already in HBM).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--op OP]
 
---op crc32 (default, the BASELINE metric) | fcs_verify (lnx_fcs_verify_batch,
+--op crc32 (default, the BASELINE metric) | fcs_append (lnx_fcs_append_batch: TX FCS
+append in place on 1496-B frames in 1536-B ring slots, lengths reset each step) | fcs_verify (lnx_fcs_verify_batch,
 residue check of the same frames) | sum16 (lnx_sum16_batch: RFC 791 checksum of
 every frame as one segment, random pseudo-header seeds) | ingress
 (lnx_ingress_verify_batch: the frames get Ethernet/IPv4/UDP headers written in
@@ -177,7 +178,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
-    ap.add_argument("--op", default="crc32", choices=["crc32", "fcs_verify", "sum16", "ingress", "rx_ring", "search"])
+    ap.add_argument("--op", default="crc32",
+                    choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search"])
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
@@ -242,6 +244,21 @@ def main():
         d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
     elif args.op == "fcs_verify":
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    elif args.op == "fcs_append":
+        # TX path (internet/stack-ethernet.go:200-214): frames of flen - 4 bytes
+        # in slots of CAP bytes get their LE FCS appended in place; the step
+        # restores the lengths first (a 4-byte-per-frame device copy, timed)
+        if flen is None:
+            raise SystemExit("--op fcs_append needs fixed-size frames")
+        cap = 1536
+        n_slots = n_local
+        d_bytes = synth.bytes_torch(n_slots * cap, dev, seed=synth.SEED + lo * 0x10001)
+        nbytes = n_slots * (flen - 4)
+        d_start = torch.arange(n_slots, dtype=torch.int64, device=dev) * cap
+        d_len0 = torch.full((n_slots,), flen - 4, dtype=torch.int32, device=dev)
+        d_len = d_len0.clone()
+        d_status = torch.empty(n_slots, dtype=torch.uint8, device=dev)
+        off_np = (np.arange(n_slots + 1, dtype=np.int64) * cap)
     elif args.op == "search":
         # PIO-capture shape (phy/rmii.md:265-271): every capture is a frame whose
         # LE FCS covers its first flen - 4 bytes, so CRC32Search scans it whole
@@ -274,6 +291,10 @@ def main():
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "search":
             L.crc32_search_batch(d_bytes, d_off, out=d_hit, stream=stream)
+        elif args.op == "fcs_append":
+            with torch.cuda.stream(stream):
+                d_len.copy_(d_len0, non_blocking=True)
+            L.fcs_append_batch(d_bytes, d_start, d_len, 1536, status=d_status, stream=stream)
         else:
             L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
 
@@ -330,6 +351,7 @@ def main():
         "sum16": "GiB/s RFC 791 internet checksum over device-resident segments; % of HBM3E read peak",
         "ingress": "GiB/s receive-path checksum verdicts (IPv4 header + UDP) over device-resident frames",
         "search": "GiB/s CRC32Search over device-resident captures (bytes scanned to the FCS hit)",
+        "fcs_append": "GiB/s TX FCS append (pad, CRC-32, LE32 store) over device-resident ring slots",
     }[args.op]
     out = {
         "metric": metric,
@@ -364,7 +386,8 @@ def main():
             "traffic": None,
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
-                       "search": "lnx::crc32_search_u_kernel<2>"}[args.op],
+                       "search": "lnx::crc32_search_u_kernel<2>",
+                       "fcs_append": "lnx::crc32_rows_kernel<kCrc> (segment mode) + pad / store"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_launches": len(timed),
             "algorithmic_bytes_per_launch": nbytes,
@@ -388,10 +411,18 @@ def main():
             got = d_ok.cpu().numpy()
         elif args.op == "search":
             got = d_hit.cpu().numpy()
+        elif args.op == "fcs_append":
+            got = d_status.cpu().numpy()
+            lens_after = d_len.cpu().numpy()
         else:
             got = d_crc.cpu().numpy().view(np.uint32)
         for i in idx:
             s, e = int(off_np[i]), int(off_np[i + 1])
+            if args.op == "fcs_append":
+                fr = d_bytes[s:s + flen].cpu().numpy().tobytes()
+                assert int(got[i]) == 0 and int(lens_after[i]) == flen, f"frame {i}: status / length"
+                assert O.crc32(fr[:-4]) == int.from_bytes(fr[-4:], "little"), f"mismatch frame {i}"
+                continue
             fr = d_bytes[s:e].cpu().numpy().tobytes()
             if args.op == "sum16":
                 want = O.payload_sum16(int(seeds[i]), fr)
@@ -423,7 +454,7 @@ def main():
         out["pcie_inclusive"] = {"value": round(nbytes / el / 2**30, 2), "unit": "GiB/s",
                                  "note": "pinned H2D of frames + kernel + D2H of CRCs, serial, 1 stream"}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op != "fcs_append":
         out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget, op=args.op)
 
     if rank == 0:

@@ -850,7 +850,10 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
 // WL = 1 runs the same slot structure on 32-lane rows (one dword per lane,
 // two frames per wave): lane p is virtual lane p, its register takes F from
 // column (p + a) mod 32, and the row XOR spans the 32 lanes.
-template <CrcMode MODE, int KS, int VAR, int WL = 2, bool JM = true, int EP = 0>
+// SEG: segment mode (frame i = bytes[start[i] : start[i] + len[i]], in address
+// order, not overlapping: ring slots, lnx_crc32_segments / the TX FCS append):
+// lanes 0..3 load the chunk's starts and lengths instead of five offsets.
+template <CrcMode MODE, int KS, int VAR, int WL = 2, bool JM = true, int EP = 0, bool SEG = false>
 __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   static_assert(WL == 1 || WL == 2, "words per lane");
   constexpr uint32_t RL = 32 / WL;  // lanes per row
@@ -869,9 +872,17 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     return b;
   };
   auto uni = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
-  // lane i < 5: low dword of off[b + i] (the range's offsets array has nfb + 1 entries)
+  // lane i < 5: low dword of off[b + i] (the range's offsets array has nfb + 1
+  // entries); SEG: lane i < 4 the low dword of start[b + i], and in bl len[b + i]
+  uint32_t bl = 0;
   auto ld_bounds = [&](uint32_t b) -> uint32_t {
-    return ld_buf<0>(b < nfb && lane <= CH ? (b + lane) * 8u : kOOB, off_rsrc);
+    if constexpr (SEG) {
+      const bool in = b + lane < nfb && lane < CH;
+      bl = ld_buf<0>(in ? (b + lane) * 4u : kOOB, cx.len_rsrc);
+      return ld_buf<0>(in ? (b + lane) * 8u : kOOB, off_rsrc);
+    } else {
+      return ld_buf<0>(b < nfb && lane <= CH ? (b + lane) * 8u : kOOB, off_rsrc);
+    }
   };
 
   // row-uniform parameters of the frame in progress
@@ -881,7 +892,8 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   auto setup = [&](uint32_t b, uint32_t bd) -> Rowp {
     Rowp r;
     const uint32_t s = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(row << 2), (int)bd);
-    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((row + 1) << 2), (int)bd);
+    const uint32_t e = SEG ? s + (uint32_t)__builtin_amdgcn_ds_bpermute((int)(row << 2), (int)bl)
+                           : (uint32_t)__builtin_amdgcn_ds_bpermute((int)((row + 1) << 2), (int)bd);
     const uint32_t f = b + row;
     const uint32_t len = e - s;
     r.f = f < nfb ? f : kNoFrame;
@@ -1150,7 +1162,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
 
   const uint32_t c0 = uni(claim());
   uint32_t bd = ld_bounds(c0);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(bd));
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(bd), "+v"(bl));
   if (c0 >= nfb) return;
   uint32_t c1 = uni(claim());
   Rowp cur = setup(c0, bd);
@@ -1162,7 +1174,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < KS; ++k) asm volatile("" : "+v"(w[k]));
-    asm volatile("" : "+v"(jk), "+v"(bd));
+    asm volatile("" : "+v"(jk), "+v"(bd), "+v"(bl));
     const Fin fin = fold(cur);
     if (c1 >= nfb) {
       finish(fin);
@@ -1232,11 +1244,11 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   // rows, 4 = lean line rows below kLeanMean, one word per lane above
   // (24-line lean items for 1600-3000 B were tried: w[24] pushed the kernel
   // past its VGPR budget into scratch)
-  bool lean = MIDW == 3 && !SEG;
+  bool lean = MIDW == 3;
   if constexpr (RLF == 0) {
     const uint64_t nf_ = fb1 - fb0, nb_ = ob1 > ob0 ? ob1 - ob0 : 0;
     rl = nf_ == 0 || nb_ < kShortMean * nf_ ? 4 : nb_ < kLineMean * nf_ ? 16 : 32;
-    if (MIDW == 4 && !SEG) lean = rl == 16 && nb_ < kLeanMean * nf_;
+    if (MIDW == 4) lean = rl == 16 && nb_ < kLeanMean * nf_;
   }
   const bool narrow = rl == 4;
   // whole-line windows: the RL = 32 image
@@ -1345,7 +1357,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     } else if (rl == 16 && lean) {
       // lean rows: 16 lanes x two words (LWL = 2) or 32 lanes x one word (LWL = 1)
       L.p = lane & (32u / LWL - 1u), L.row = lane / (32u / LWL);
-      if constexpr (!SEG) lines_body<MODE, KSL, VAR, LWL, LJM, LEP>(lds, L, cx);
+      lines_body<MODE, KSL, VAR, LWL, LJM, LEP, SEG>(lds, L, cx);
     } else if (rl == 16) {
       L.p = lane & 15u, L.row = lane >> 4;
       rows_body<MODE, 16, KSM, SM, CHM, VAR, SEG, MIDW == 2 ? 2 : 1, true, MIDW == 2 ? 0 : NSR4>(lds, L, cx);
