@@ -478,7 +478,7 @@ crc32_search_half_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __re
 // lane carries NC independent Z_4 chains through pass A and pass B (one 16-wave
 // block per CU leaves four waves per SIMD to hide the LDS latency; r2s2e: one
 // capture per half ran 0.666 ms against 0.624 for the two-block form).
-template <int NC, bool SPLIT = false>
+template <int NC, bool SPLIT = false, int GLD = 1>
 __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __restrict__ bytes,
                                               const uint64_t* __restrict__ off, const int64_t* __restrict__ min_off,
                                               uint64_t n, const uint32_t* __restrict__ tables,
@@ -516,9 +516,31 @@ __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __re
       g.m[j] = lv && min_off ? min_off[cc] : 0;
     }
   };
-  // the words of block B of each capture of a group (only dwords holding a capture byte)
+  // the words of block B of each capture of a group (only dwords holding a capture byte).
+  // Packed groups (every capture of the group inside [off[first], off[last + 1]),
+  // under 2 GiB) load through one buffer descriptor over the group's bytes
+  // instead: one per-lane offset, the word index in the immediate, no guard
+  // (words past a capture's end are the next capture's bytes and only feed
+  // states past its end; past the group the range check returns 0).
+  __amdgpu_buffer_rsrc_t grsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes), (short)0, 0, 0x00020000);
+  uint64_t gbase = 0;
+  bool gfast = false;
   auto load_words = [&](const Grp& g, int64_t B, const bool (&ac)[NC], uint32_t (&v)[NC][NW + 1]) {
     const int64_t base = B + (int64_t)(SEG * hl);
+    if (gfast) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const uint64_t a = g.s[j] + (uint64_t)base;  // byte offset of the lane's segment in `bytes`
+        const uint32_t vo = ac[j] ? (uint32_t)((a & ~3ull) - gbase) : 0x80000000u;
+        // GLD 2: alternate the nt bit so hipcc cannot merge neighbours into
+        // 16-byte loads (GLD 1 lets it)
+#pragma unroll
+        for (uint32_t i = 0; i <= NW; ++i)
+          v[j][i] = GLD == 2 && (i & 1) ? __builtin_amdgcn_raw_buffer_load_b32(grsrc, vo + 4 * i, 0, 2)
+                                        : __builtin_amdgcn_raw_buffer_load_b32(grsrc, vo + 4 * i, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       const uint8_t* dj = bytes + g.s[j];
@@ -546,6 +568,29 @@ __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __re
     uint32_t carry[NC];
     Grp gc;
     load_grp(q, gc);
+    {
+      // the group's byte range (wave-uniform: off[] of the group's first and one-past-last capture)
+      const uint64_t ga = q * CPW, gb = ga + CPW < n ? ga + CPW : n;
+      const uint64_t gs = off[ga], ge = off[gb];
+      bool inside = ge >= gs && ge - (gs & ~3ull) + 3 < (1ull << 31);
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        inside = inside && (gc.e[j] <= gc.s[j] || (gc.s[j] >= gs && gc.e[j] <= ge));
+      gfast = GLD != 0 && __builtin_amdgcn_ballot_w64(!inside) == 0;
+      // gs / ge are wave-uniform (one group per wave): move them to SGPRs, or
+      // hipcc wraps every buffer load in a waterfall loop over the descriptor
+      auto uni64 = [](uint64_t x) -> uint64_t {
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
+      };
+      gbase = uni64(gs) & ~3ull;
+      const uint64_t geu = uni64(ge);
+      grsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes + gbase), (short)0,
+                                                // rounded up to whole dwords: the range check drops a dword
+                                                // that straddles the end, and the one holding the group's
+                                                // last byte never crosses a page
+                                                gfast ? (int)((geu - gbase + 3) & ~3ull) : 0, 0x00020000);
+    }
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       c[j] = q * CPW + 2 * j + half;
@@ -687,7 +732,7 @@ __device__ __forceinline__ void search_u_body(uint32_t* lds, const uint8_t* __re
   }
 }
 
-template <int NC, bool SPLIT = false>
+template <int NC, bool SPLIT = false, int GLD = 1>
 __global__ void __launch_bounds__(kSegBlock, 1)
 crc32_search_u_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                       const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
@@ -696,7 +741,7 @@ crc32_search_u_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
   if constexpr (NC == 0)
     search_half_body<12, true, 0, true>(lds, bytes, off, min_off, n, tables, result);
   else
-    search_u_body<NC, SPLIT>(lds, bytes, off, min_off, n, tables, result);
+    search_u_body<NC, SPLIT, GLD>(lds, bytes, off, min_off, n, tables, result);
 }
 
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
@@ -795,6 +840,15 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
         const uint64_t g1 = g2 < (uint64_t)num_cus ? g2 : (uint64_t)num_cus;
         hipLaunchKernelGGL((crc32_search_u_kernel<1, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
+      } else if (mode == 'g' || mode == 'G') {  // product with the guarded global loads (g) / unmerged group loads (G)
+        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
+        if (mode == 'g')
+          hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 0>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
+                             bytes, off, min_off, n, tables, result);
+        else
+          hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 2>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
+                             bytes, off, min_off, n, tables, result);
       } else if (mode == 'q') {  // U layout, two captures per half, each segment as two 24-byte chains
         uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
         if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
