@@ -21,7 +21,7 @@ import os
 __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
-    "crc32_batch_host", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE", "RxRing",
+    "crc32_batch_host", "crc32_batch_multi", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE", "RxRing",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -196,7 +196,12 @@ class _Batch:
         import torch
         self.what = what
         dev = None
+        # a kind ending in "?" marks an optional argument (NULL in the C-ABI)
         for name, t, kind in args:
+            if t is None and not kind.endswith("?"):
+                raise LnetoError(f"{what}: {name} is required")
+        for name, t, kind in args:
+            kind = kind.rstrip("?")
             if t is None:
                 continue
             if not isinstance(t, torch.Tensor) or not t.is_cuda or not t.is_contiguous():
@@ -311,7 +316,7 @@ def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
     (lnx_crc32_search_batch).  d_min_off: int64 (N) or None.  Returns int64 (N), -1 = none."""
     import torch
     what = "lnx_crc32_search_batch"
-    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64"), ("d_min_off", d_min_off, "i64")],
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64"), ("d_min_off", d_min_off, "i64?")],
                stream)
     n = d_off.numel() - 1
     _need_len(what, "d_min_off", d_min_off, n)
@@ -350,7 +355,7 @@ def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):
     import torch
     what = "lnx_sum16_batch"
     b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64"), ("d_len", d_len, "i32"),
-                      ("d_seed", d_seed, "i32")], stream)
+                      ("d_seed", d_seed, "i32?")], stream)
     n = d_off.numel()
     _need_len(what, "d_len", d_len, n)
     _need_len(what, "d_seed", d_seed, n)
@@ -361,6 +366,33 @@ def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):
                                        d_seed.data_ptr() if d_seed is not None else None, n,
                                        out.data_ptr(), s), what)
     return out
+
+
+def crc32_batch_multi(parts, devices):
+    """lnx_crc32_batch_multi: one host thread per entry of ``devices``; part g is
+    a (d_bytes, d_off) pair on device ``devices[g]`` (offsets local to its own
+    buffer).  Synchronous; returns one int32 CRC tensor per part.  The same
+    device may appear more than once (a one-GPU rehearsal of the partition)."""
+    import torch
+    what = "lnx_crc32_batch_multi"
+    if len(parts) != len(devices) or not parts:
+        raise LnetoError(f"{what}: one (d_bytes, d_off) part per device")
+    outs = []
+    for g, (d_bytes, d_off) in enumerate(parts):
+        b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], None)
+        if b.device.index != devices[g]:
+            raise LnetoError(f"{what}: part {g} is on {b.device}, devices[{g}] = {devices[g]}")
+        outs.append(torch.empty(max(d_off.numel() - 1, 0), dtype=torch.int32, device=b.device))
+    ng = len(parts)
+    devs = (ctypes.c_int * ng)(*devices)
+    bp = (ctypes.c_void_p * ng)(*[p[0].data_ptr() for p in parts])
+    op = (ctypes.c_void_p * ng)(*[p[1].data_ptr() for p in parts])
+    ns = (ctypes.c_uint64 * ng)(*[max(p[1].numel() - 1, 0) for p in parts])
+    cp = (ctypes.c_void_p * ng)(*[o.data_ptr() for o in outs])
+    for d in set(devices):  # the library's threads use the null stream: order after torch's work
+        torch.cuda.synchronize(d)
+    _check(lib.lnx_crc32_batch_multi(ng, devs, bp, op, ns, cp), what)
+    return outs
 
 
 def crc32_batch_host(h_bytes, h_off, device: int = 0):

@@ -1385,16 +1385,10 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
                      timeline, seg_len)
   if (seg_len) {  // segment mode (lnx_crc32_segments, the TX FCS append, the receive ring)
-    // profiling: LNX_PROF_SEG_EP=0 loads every lean-row step non-temporally
-    // (slots share no line with their neighbours; EP = 1 is the product)
-    static const int seg_ep = [] {
-      const char* e = getenv("LNX_PROF_SEG_EP");
-      return e ? atoi(e) : 1;
-    }();
+    // (every lean-row step non-temporal, EP = 0, was measured no faster for
+    // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
     if (verify)
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
-    else if (seg_ep == 0)
-      LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true, 4, 24, 1, 4, 13, 2, true, 0);
     else
       LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true);
   } else if (verify) {

@@ -230,6 +230,18 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       // la <= 74. There the transport mask is the end bound alone and the
       // header sum takes nothing.
       const int32_t qend = (kend + 1) >> 1;
+      // The first batch was loaded up to the frame end (qfend), before the
+      // header parse knew the transport end: its qwords at or past qend (bytes
+      // after tl, after the UDP length, after pl + 40) are not summed.  Only
+      // rows whose frame runs past the transport end take this branch.
+      if (qend < qfend) {
+#pragma unroll
+        for (int u = 1; u < UNR; ++u) {
+          const bool past = qstart + (int32_t)p + 16 * u >= qend;
+          y[u].x = past ? 0u : y[u].x;
+          y[u].y = past ? 0u : y[u].y;
+        }
+      }
       bool first = true;
       uint2 yl = make_uint2(0u, 0u);  // the row's last qword, on the lane that loaded it (outside the first qwords)
       for (int32_t q0 = qstart + (int32_t)p; q0 < qend; q0 += 16 * UNR) {
@@ -254,10 +266,11 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
               tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
             } else {
-              // summed whole: only the row's last loaded qword (qend - 1) can
-              // hold bytes at or past lb (every earlier one ends at or before
-              // it); the lane holding it keeps it and takes those bytes back
-              // out after the loop
+              // summed whole: every qword here lies below qend (later batches
+              // load under q < qend; the first batch's qwords at or past qend
+              // were zeroed above), so only qword qend - 1 can hold bytes at
+              // or past lb; the lane holding it keeps it and takes those bytes
+              // back out after the loop
               tE = __builtin_amdgcn_udot4(w, wE, tE, false);
               tO = __builtin_amdgcn_udot4(w, wO, tO, false);
             }

@@ -69,6 +69,44 @@ def short_tcp6(rng) -> bytes:
     return bytes(raw)
 
 
+def trailing_frames(seed: int = 7, count: int = 600) -> list[bytes]:
+    """Frames whose transport data ends before the frame does, followed by
+    non-zero bytes the receive path must ignore: IPv4 TCP / UDP with bytes past
+    tl (internet/stack-ip4.go:100-107 slices the frame to tl), IPv4 UDP whose
+    UDP length is below the IP payload (the sum covers ufrm.RawData()[:Length()],
+    stack-ip4.go:161-163), and IPv6 with bytes past pl + 40 (ipv6 payload is
+    sliced by PayloadLength, stack-ip6.go:86-138).  Transport payloads of
+    150-1200 B so the ignored bytes land in the middle of a row's batch;
+    a third of the frames carry one flipped byte inside the covered range."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        n = int(rng.integers(150, 1200))
+        pay = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        tail = (rng.integers(1, 256, size=int(rng.integers(16, 300)), dtype=np.uint8)).tobytes()
+        kind = i % 5
+        if kind == 0:
+            f = ether(0x0800, ipv4(6, tcp(pay))) + tail
+        elif kind == 1:
+            f = ether(0x0800, ipv4(17, udp(pay))) + tail
+        elif kind == 2:  # UDP length < IP payload: the rest of the IP payload is outside the sum
+            ul = 8 + int(rng.integers(0, n))
+            f = ether(0x0800, ipv4(17, udp(pay, length=ul)))
+        elif kind == 3:
+            f = ether(0x86DD, ipv6(6, tcp(pay))) + tail
+        else:
+            f = ether(0x86DD, ipv6(17, udp(pay))) + tail
+        if i % 3 == 0:
+            b = bytearray(f)
+            end = 14 + (struct.unpack(">H", b[16:18])[0] if kind < 3 else 40 + struct.unpack(">H", b[18:20])[0])
+            if kind == 2:
+                end = 14 + 20 + struct.unpack(">H", b[38:40])[0]
+            b[int(rng.integers(min(60, end - 1), end))] ^= 0x04
+            f = bytes(b)
+        out.append(f)
+    return out
+
+
 def frames(seed: int = 1, count: int = 3000) -> list[bytes]:
     """A mixed batch: valid frames of every kind plus every malformation the
     receive path distinguishes, with random payload sizes (odd ones too)."""

@@ -17,6 +17,17 @@ def test_host_tensors_rejected():
         L.sum16_batch(d, o[:2].contiguous(), torch.tensor([4, 4], dtype=torch.int32))
 
 
+def test_required_none_rejected():
+    """Only the optional arguments (d_min_off, d_seed) may be None."""
+    o = torch.tensor([0, 4, 8], dtype=torch.int64)
+    with pytest.raises(L.LnetoError, match="d_bytes is required"):
+        L.crc32_batch(None, o)
+    with pytest.raises(L.LnetoError, match="d_off is required"):
+        L.crc32_search_batch(torch.zeros(8, dtype=torch.uint8), None)
+    with pytest.raises(L.LnetoError, match="d_len is required"):
+        L.sum16_batch(torch.zeros(8, dtype=torch.uint8), o, None)
+
+
 @pytest.mark.gpu
 def test_wrong_widths_rejected(cuda):
     d = torch.zeros(64, dtype=torch.uint8, device=cuda)

@@ -125,6 +125,33 @@ def test_gpu_ingress_reference_frames(cuda):
     assert got.tolist() == [0, 0, 0, O.ERR_BAD_CRC]
 
 
+def test_trailing_bytes_are_ignored():
+    """Bytes past the transport end never reach a sum (the reference slices the
+    frame to tl / the UDP length / pl + 40 before summing): valid frames pass
+    whatever follows them, and a flip inside the covered range is ErrBadCRC."""
+    frames = G.trailing_frames(count=300)
+    for i, f in enumerate(frames):
+        want = O.ERR_BAD_CRC if i % 3 == 0 else 0
+        assert O.ingress_verdict(f) == want, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base_pad", [0, 1, 6])
+def test_gpu_ingress_trailing_bytes(cuda, base_pad):
+    """ADVICE r2 (high): the first batch of qwords is loaded to the frame end;
+    the ones past the transport end must not be summed."""
+    import torch
+    import lneto_amd as L
+    frames = G.trailing_frames(seed=40 + base_pad, count=1200)
+    data, off = _pack(frames, base_pad)
+    got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda),
+                                 torch.from_numpy(off.astype(np.int64)).to(cuda)).cpu().numpy()
+    want = np.array([O.ingress_verdict(f) for f in frames], dtype=np.uint8)
+    assert (want == 0).sum() > 600
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
+
+
 def _header_then_udp_frames():
     """Corrupted IPv4 header AND a broken UDP size: demux4 checks the header sum
     (internet/stack-ip4.go:128-131) before udp.NewFrame / ValidateSize (:150-158),

@@ -108,6 +108,48 @@ def test_two_captures_per_wave_pairs(cuda):
     assert not bad, [(i, len(caps[i]), mins[i], got[i], want[i]) for i in bad[:10]]
 
 
+def test_decreasing_offsets_take_the_guarded_loads(cuda):
+    """a group of four captures that do not all lie inside
+    [off[4q], off[4q + 4]) cannot use the group buffer descriptor and takes the
+    per-capture guarded loads (search_kernel.hip, gfast false).  Captures laid
+    out in reverse order: off = [a0, b0, a1, b1, ...] with a_{k+1} < b_k, so
+    capture 2k = [a_k, b_k) is real and capture 2k + 1 (end below start) is
+    empty, -1 (ethernet/crc.go:29-34)."""
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(24)
+    caps = []
+    for i in range(600):
+        body = rng.integers(0, 256, size=int(rng.integers(0, 1800)), dtype=np.uint8).tobytes()
+        if i % 4 != 3:
+            cut = int(rng.integers(0, len(body) + 1))
+            body = body[:cut] + struct.pack("<I", O.crc32(body[:cut])) + body[cut:cut + int(rng.integers(0, 40))]
+        caps.append(body)
+    pad = 3
+    blob = bytearray(b"\x5a" * pad)
+    pos = {}
+    for k in reversed(range(len(caps))):  # capture k sits before capture k - 1 in memory
+        pos[k] = len(blob)
+        blob += caps[k] + bytes(int(rng.integers(0, 5)))
+    blob += b"\0" * 8
+    offs, want, mins = [], [], []
+    for k, c in enumerate(caps):
+        offs += [pos[k], pos[k] + len(c)]
+    offs = np.array(offs, dtype=np.int64)
+    for i in range(len(offs) - 1):
+        s, e = int(offs[i]), int(offs[i + 1])
+        cap = bytes(blob[s:e]) if e > s else b""
+        m = int(rng.choice([0, 1, len(cap) // 2]))
+        mins.append(m)
+        want.append(O.crc32_search(cap, m))
+    assert sum(w >= 0 for w in want) > 300
+    d = torch.from_numpy(np.frombuffer(bytes(blob), dtype=np.uint8).copy()).to(cuda)
+    got = L.crc32_search_batch(d, torch.from_numpy(offs).to(cuda),
+                               torch.tensor(mins, dtype=torch.int64, device=cuda)).cpu().numpy().tolist()
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, [(i, got[i], want[i]) for i in bad[:10]]
+
+
 @pytest.mark.parametrize("count", [1, 2, 3, 5, 6, 7, 257])
 def test_four_captures_per_wave_groups(cuda, count):
     """crc32_search_u_kernel<2> folds captures 4q .. 4q + 3 in one wave (two
