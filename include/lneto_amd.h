@@ -107,6 +107,28 @@ int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const ui
 int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
                          uint8_t* d_status, void* stream);
 
+/* Batched transmit checksum generate: for every
+ * frame d_bytes[d_start[i] : d_start[i] + d_len[i]] — an Ethernet header and
+ * the IP packet a stack child just wrote, before padding and FCS — the step
+ * encapsulate4 / encapsulate6 and the ICMP clients run after the child
+ * (internet/stack-ip4.go:202-228, internet/stack-ip6.go:167-181,
+ * ipv4/icmpv4/client.go:210-214, ipv6/icmpv6/client.go:135-148), in place:
+ *   IPv4: total length = len - 14; header CRC over the first 20 bytes
+ *         (ipv4/frame.go:138-146); TCP CRC with CRCWriteTCPPseudo; UDP length
+ *         = n and UDP CRC with CRCWriteUDPPseudo(n) through NeverZeroSum
+ *         (crc.go:65-71); ICMP CRC over the message with a zero seed;
+ *   IPv6: payload length = len - 54; TCP / UDP / ICMPv6 CRC with
+ *         CRCWritePseudo (ipv6/frame.go:104-108), UDP length = n, NeverZeroSum
+ *         for UDP.
+ * The header length is the frame's own IHL.  d_status[i] = 0 when done (other
+ * EtherTypes and IP protocols: nothing, or the IPv4 header CRC / the IPv6
+ * payload length only), else the frame is untouched and d_status[i] = 18
+ * (lneto.ErrTruncatedFrame: too short for the IP header or for the TCP 20 /
+ * UDP 8 / ICMP 8-byte header the step writes) or 15 (ErrInvalidLengthField:
+ * IHL < 5, or a length over 16 bits).  Frames must not overlap. */
+int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
+                          uint8_t* d_status, void* stream);
+
 /* FCS verify of received frames that still carry their 4-byte LE FCS:
  * d_ok[i] = 1 iff len_i >= 4 and CRC32(f[:len_i-4]) == LE32(f[len_i-4:]),
  * evaluated as the residue test CRC32(f) == LNX_CRC32_RESIDUE.  This is the

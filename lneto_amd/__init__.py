@@ -21,7 +21,8 @@ import os
 __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
-    "crc32_batch_host", "crc32_batch_multi", "device_count", "version", "LIB_PATH", "CRC32_RESIDUE", "RxRing",
+    "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "LIB_PATH",
+    "CRC32_RESIDUE", "RxRing",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -71,6 +72,7 @@ _sig = {
     "lnx_crc32_search_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_crc32_segments": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_fcs_append_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
+    "lnx_tx_checksum_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_crc32_batch_host": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
     "lnx_crc32_batch_multi": (ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     "lnx_rx_ring_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -308,6 +310,24 @@ def fcs_append_batch(d_bytes, d_start, d_len, capacity: int, status=None, stream
         with b as s:
             _check(lib.lnx_fcs_append_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n, capacity,
                                             status.data_ptr(), s), what)
+    return status
+
+
+def tx_checksum_batch(d_bytes, d_start, d_len, status=None, stream=None):
+    """Transmit checksum generate in place (lnx_tx_checksum_batch): IPv4 / IPv6
+    length fields, IPv4 header CRC, TCP / UDP / ICMP CRCs of every frame
+    d_bytes[d_start[i] : d_start[i] + d_len[i]] (int64 starts, int32 lengths).
+    Returns the uint8 status (0, 18 ErrTruncatedFrame, 15 ErrInvalidLengthField)."""
+    import torch
+    what = "lnx_tx_checksum_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_start", d_start, "i64"), ("d_len", d_len, "i32")], stream)
+    n = d_start.numel()
+    _need_len(what, "d_len", d_len, n)
+    status = _out(what, status, n, torch.uint8, "u8", b.device)
+    if n > 0:
+        with b as s:
+            _check(lib.lnx_tx_checksum_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n,
+                                             status.data_ptr(), s), what)
     return status
 
 

@@ -69,11 +69,23 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
 // QW: lanes load qwords (global_load_dwordx2: a 16-lane row reads a whole
 // 128-byte line per instruction), UNR qwords per lane in flight; otherwise
 // dwords (a 64-byte half line per row instruction), UNR dwords in flight
-template <int UNR, bool QW>
+//
+// GEN (tx_checksum_batch): the same rows GENERATE the
+// checksums instead (encapsulate4 / encapsulate6 / the ICMP clients after the
+// child wrote its n payload bytes, internet/stack-ip4.go:202-228,
+// internet/stack-ip6.go:167-181, ipv4/icmpv4/client.go:210-214,
+// ipv6/icmpv6/client.go:135-148): the length fields are set from the frame
+// length, and the sums are taken over the bytes as loaded with the old field
+// values subtracted (uint32 wrap: the same value as summing with the fields
+// zeroed); lanes 0..7 of the row then store the 2-byte fields (IPv4 total
+// length / IPv6 payload length, header CRC, transport CRC, UDP length) and
+// `verdict` receives the status (0, or 18 / 15 with the frame untouched).
+template <int UNR, bool QW, bool GEN = false>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
                       uint32_t trim) {
+  static_assert(!GEN || QW, "generate runs on the qword rows");
   // offsets mode (seg_len null): frame f = bytes[off[f] : off[f+1]]; segment
   // mode (the receive ring): frame f = bytes[off[f] : off[f] + seg_len[f] - trim],
   // i.e. the FCS (trim = 4) is stripped, empty if seg_len[f] < trim
@@ -146,68 +158,133 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     bool hdr_sum = false, l4_sum = false;
     int32_t pa = 0, pb = 0, la = 0, lb = 0;  // pseudo-address bytes [pa, pb), transport [la, lb)
     uint32_t lseed = 0;                       // length + protocol words of the pseudo-header
-    if (L < 14) {
-      v = kErrTruncatedFrame;
-    } else {
-      const uint32_t et = be(H0, 0);
-      if (et <= 1500 && L < et) {
-        v = kErrInvalidLengthField;
-      } else if (et == 0x8100 && L < 18) {
+    // GEN: the fields the step writes (frame offset, new value; 0 = none)
+    uint32_t g_off[4] = {0, 0, 0, 0}, g_val[4] = {0, 0, 0, 0};
+    uint32_t g_fix_h = 0, g_fix_t = 0;  // new - old of the summed fields (header, transport), mod 2^32
+    bool g_nz = false;                   // UDP: NeverZeroSum (crc.go:65-71)
+    if constexpr (GEN) {
+      if (L < 14) {
         v = kErrTruncatedFrame;
-      } else if (et == 0x0800) {
-        const uint32_t M = L - 14;
-        if (M < 20) {
-          v = kErrTruncatedFrame;
-        } else {
-          const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
-          if (tl < 20) v = kErrInvalidLengthField;
-          else if (tl > M) v = kErrTruncatedFrame;
-          else if (ihl < 5 || ihl * 4 > tl) v = kErrInvalidLengthField;
-          else if ((b0 >> 4) != 4) v = kErrInvalidField;
-          else if ((flags & kVerifyEvilBit) && (be(H2, 0) & (1u << 13))) v = kErrPacketDrop;
+      } else {
+        const uint32_t et = be(H0, 0);
+        if (et == 0x0800) {
+          const uint32_t ihl = byt(H0, 2) & 15u, hl = 4 * ihl;
+          if (L < 34) v = kErrTruncatedFrame;
+          else if (ihl < 5) v = kErrInvalidLengthField;
+          else if (14 + hl > L) v = kErrTruncatedFrame;
+          else if (L - 14 > 0xFFFFu) v = kErrInvalidLengthField;
           if (v == 0) {
-            hdr_sum = true;
-            const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
-            if (proto == 6) {
-              l4_sum = true;
-              pa = 26, pb = 34, la = 14 + hl, lb = 14 + tl;
-              lseed = ((tl - hl) & 0xFFFFu) + 6u;
-            } else if (proto == 17) {
-              if (P < 8) {
-                v_udp4 = kErrTruncatedFrame;
-              } else {
-                const uint32_t ul = field16(14 + hl + 4);
-                if (ul < 8) v_udp4 = kErrInvalidLengthField;
-                else if (ul > P) v_udp4 = kErrTruncatedFrame;
-                else {
-                  l4_sum = true;
-                  pa = 26, pb = 34, la = 14 + hl, lb = 14 + hl + ul;
-                  lseed = ul + 17u;
+            const uint32_t tl = L - 14, nn = tl - hl, proto = byt(H2, 3);
+            const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 1) ? 8u : 0u;
+            if (nn < need) v = kErrTruncatedFrame;
+            if (v == 0) {
+              hdr_sum = true;
+              g_off[0] = 16, g_val[0] = tl;   // SetTotalLength(n + hl)
+              g_off[1] = 24;                  // SetCRC(CalculateHeaderCRC()), value after the sums
+              g_fix_h = tl - be(H1, 0) - field16(24);
+              if (need) {
+                l4_sum = true;
+                la = 14 + hl, lb = L;
+                const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
+                g_off[2] = la + at;
+                g_fix_t = 0u - field16(la + at);
+                if (proto != 1) pa = 26, pb = 34, lseed = nn + proto;  // CRCWriteTCPPseudo / CRCWriteUDPPseudo(n)
+                if (proto == 17) {
+                  g_off[3] = la + 4, g_val[3] = nn;  // SetLength(n)
+                  g_fix_t += nn - field16(la + 4);
+                  g_nz = true;
                 }
               }
             }
           }
-        }
-      } else if (et == 0x86DD) {
-        const uint32_t M = L - 14;
-        if (M < 40) {
-          v = kErrTruncatedFrame;
-        } else {
-          const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
-          if (pl + 40 > M) {
-            v = kErrInvalidLengthField;
-          } else if (proto == 6 || proto == 17) {
-            // demux6 size-checks the UDP header only; TCP goes straight to the
-            // sum (internet/stack-ip6.go:116-137), whatever pl is.
-            if (proto == 17) {
-              if (pl < 8) v = kErrTruncatedFrame;
-              else if (field16(58) < 8) v = kErrInvalidLengthField;
-              else if (field16(58) > pl) v = kErrTruncatedFrame;
-            }
-            if (v == 0) {
+        } else if (et == 0x86DD) {
+          const uint32_t nn = L - 54, proto = byt(H2, 0);
+          if (L < 54) v = kErrTruncatedFrame;
+          else if (nn > 0xFFFFu) v = kErrInvalidLengthField;
+          const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 58) ? 8u : 0u;
+          if (v == 0 && nn < need) v = kErrTruncatedFrame;
+          if (v == 0) {
+            g_off[0] = 18, g_val[0] = nn;  // SetPayloadLength(n)
+            if (need) {
               l4_sum = true;
-              pa = 22, pb = 54, la = 54, lb = 54 + pl;  // AddUint32(pl), AddUint32(proto): high halves 0
-              lseed = pl + proto;
+              pa = 22, pb = 54, la = 54, lb = L;  // CRCWritePseudo: AddUint32(n), AddUint32(proto)
+              lseed = nn + proto;
+              const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
+              g_off[2] = 54 + at;
+              g_fix_t = 0u - field16(54 + at);
+              if (proto == 17) {
+                g_off[3] = 58, g_val[3] = nn;
+                g_fix_t += nn - field16(58);
+                g_nz = true;
+              }
+            }
+          }
+        }
+      }
+    } else {
+      if (L < 14) {
+        v = kErrTruncatedFrame;
+      } else {
+        const uint32_t et = be(H0, 0);
+        if (et <= 1500 && L < et) {
+          v = kErrInvalidLengthField;
+        } else if (et == 0x8100 && L < 18) {
+          v = kErrTruncatedFrame;
+        } else if (et == 0x0800) {
+          const uint32_t M = L - 14;
+          if (M < 20) {
+            v = kErrTruncatedFrame;
+          } else {
+            const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
+            if (tl < 20) v = kErrInvalidLengthField;
+            else if (tl > M) v = kErrTruncatedFrame;
+            else if (ihl < 5 || ihl * 4 > tl) v = kErrInvalidLengthField;
+            else if ((b0 >> 4) != 4) v = kErrInvalidField;
+            else if ((flags & kVerifyEvilBit) && (be(H2, 0) & (1u << 13))) v = kErrPacketDrop;
+            if (v == 0) {
+              hdr_sum = true;
+              const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
+              if (proto == 6) {
+                l4_sum = true;
+                pa = 26, pb = 34, la = 14 + hl, lb = 14 + tl;
+                lseed = ((tl - hl) & 0xFFFFu) + 6u;
+              } else if (proto == 17) {
+                if (P < 8) {
+                  v_udp4 = kErrTruncatedFrame;
+                } else {
+                  const uint32_t ul = field16(14 + hl + 4);
+                  if (ul < 8) v_udp4 = kErrInvalidLengthField;
+                  else if (ul > P) v_udp4 = kErrTruncatedFrame;
+                  else {
+                    l4_sum = true;
+                    pa = 26, pb = 34, la = 14 + hl, lb = 14 + hl + ul;
+                    lseed = ul + 17u;
+                  }
+                }
+              }
+            }
+          }
+        } else if (et == 0x86DD) {
+          const uint32_t M = L - 14;
+          if (M < 40) {
+            v = kErrTruncatedFrame;
+          } else {
+            const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
+            if (pl + 40 > M) {
+              v = kErrInvalidLengthField;
+            } else if (proto == 6 || proto == 17) {
+              // demux6 size-checks the UDP header only; TCP goes straight to the
+              // sum (internet/stack-ip6.go:116-137), whatever pl is.
+              if (proto == 17) {
+                if (pl < 8) v = kErrTruncatedFrame;
+                else if (field16(58) < 8) v = kErrInvalidLengthField;
+                else if (field16(58) > pl) v = kErrTruncatedFrame;
+              }
+              if (v == 0) {
+                l4_sum = true;
+                pa = 22, pb = 54, la = 54, lb = 54 + pl;  // AddUint32(pl), AddUint32(proto): high halves 0
+                lseed = pl + proto;
+              }
             }
           }
         }
@@ -310,9 +387,21 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       }
     }
     hE = row_add(hE), hO = row_add(hO), tE = row_add(tE), tO = row_add(tO);
-    if (v == 0 && hdr_sum && ing_sum16(256u * hE + hO) != 0) v = kErrBadCRC;
-    if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
-    if (v == 0 && l4_sum && ing_sum16(256u * tE + tO + lseed) != 0) v = kErrBadCRC;
+    if constexpr (GEN) {
+      g_val[1] = ing_sum16(256u * hE + hO + g_fix_h);
+      const uint32_t tc = ing_sum16(256u * tE + tO + lseed + g_fix_t);
+      g_val[2] = g_nz && tc == 0 ? 0xFFFFu : tc;
+      // lane p stores byte p & 1 (big-endian) of field p >> 1
+      const uint32_t k = p >> 1;
+      const uint32_t fo = k == 0 ? g_off[0] : k == 1 ? g_off[1] : k == 2 ? g_off[2] : g_off[3];
+      const uint32_t fv = k == 0 ? g_val[0] : k == 1 ? g_val[1] : k == 2 ? g_val[2] : g_val[3];
+      if (live && v == 0 && k < 4 && fo != 0)
+        const_cast<uint8_t*>(fr)[fo + (p & 1u)] = (uint8_t)((p & 1u) ? fv : fv >> 8);
+    } else {
+      if (v == 0 && hdr_sum && ing_sum16(256u * hE + hO) != 0) v = kErrBadCRC;
+      if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
+      if (v == 0 && l4_sum && ing_sum16(256u * tE + tO + lseed) != 0) v = kErrBadCRC;
+    }
     if (live && p == 0) verdict[f] = (uint8_t)v;
   }
 }
@@ -351,6 +440,21 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   else
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream,
                        bytes, off, n, flags, verdict, seg_len, trim);
+  return hipGetLastError();
+}
+
+// Batched transmit checksum generate over ring slots: frame i =
+// bytes[start[i] : start[i] + len[i]] (segment mode, trim 0), status[i] as
+// lnx_tx_checksum_batch documents.
+hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                              uint8_t* status, int num_cus, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t frames_per_block = (kIngBlock / 64) * 4;
+  uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
+  const uint64_t cap = (uint64_t)num_cus * 128;
+  if (grid > cap) grid = cap;
+  hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, true>), dim3((unsigned)grid), dim3(kIngBlock), 0,
+                     stream, bytes, start, n, 0u, status, len, 0u);
   return hipGetLastError();
 }
 

@@ -275,6 +275,95 @@ def ingress_verdict(frame: bytes, flags: int = 0) -> int:
     return 0
 
 
+# ------------------------------------------------- TX checksum generate (a16)
+IPPROTO_ICMP = 1
+IPPROTO_ICMPV6 = 58
+
+
+def _put16(b: bytearray, i: int, v: int) -> None:
+    b[i:i + 2] = struct.pack(">H", v & 0xFFFF)
+
+
+def tx_checksum(frame: bytes) -> tuple[bytes, int]:
+    """The checksum-generate step of the transmit path for one Ethernet frame
+    (Ethernet header + IP packet, before padding and FCS), as encapsulate4 /
+    encapsulate6 and the ICMP clients run it once the child has written its
+    n-byte payload:
+
+    IPv4 (internet/stack-ip4.go:202-228): SetTotalLength(n + hl); SetCRC(0);
+      SetCRC(CalculateHeaderCRC()) (first 20 bytes only, ipv4/frame.go:138-146);
+      TCP: CRCWriteTCPPseudo, tcp SetCRC(0), SetCRC(PayloadSum16(payload));
+      UDP: CRCWriteUDPPseudo(n), SetLength(n), SetCRC(0),
+           SetCRC(NeverZeroSum(PayloadSum16(payload))) (crc.go:65-71);
+      ICMP (ipv4/icmpv4/client.go:210-214): SetCRC(0), SetCRC(CRC791{}.PayloadSum16(msg)).
+    IPv6 (internet/stack-ip6.go:167-181): SetPayloadLength(n); TCP / UDP as
+      above with CRCWritePseudo (ipv6/frame.go:104-108); ICMPv6
+      (ipv6/icmpv6/client.go:135-148): SetCRC(0), WriteEven(src, dst),
+      AddUint32(n), AddUint32(58), PayloadSum16(msg).
+    The header length is the frame's own IHL (encapsulate4 writes 5).
+    Returns (new frame, status): 0 when written (other EtherTypes / protocols
+    are left as they are), else the frame unchanged with ErrTruncatedFrame (18)
+    when it is too short for a header the step writes (ipv4.NewFrame, tcp /
+    udp / icmp NewFrame: 20, 20, 8, 8 bytes; the reference would panic on the
+    transport ones, whose error it discards) or ErrInvalidLengthField (15) for
+    IHL < 5 or a length that does not fit 16 bits."""
+    f = bytearray(frame)
+    if len(f) < 14:
+        return bytes(frame), ERR_TRUNCATED_FRAME
+    et = _be16(f, 12)
+    if et == ETHERTYPE_IPV4:
+        if len(f) < 34:
+            return bytes(frame), ERR_TRUNCATED_FRAME
+        hl = (f[14] & 0xF) * 4
+        if hl < 20:
+            return bytes(frame), ERR_INVALID_LENGTH_FIELD
+        if 14 + hl > len(f):
+            return bytes(frame), ERR_TRUNCATED_FRAME
+        tl = len(f) - 14
+        if tl > 0xFFFF:
+            return bytes(frame), ERR_INVALID_LENGTH_FIELD
+        n, proto, la = tl - hl, f[23], 14 + hl
+        need = {IPPROTO_TCP: 20, IPPROTO_UDP: 8, IPPROTO_ICMP: 8}.get(proto, 0)
+        if n < need:
+            return bytes(frame), ERR_TRUNCATED_FRAME
+        _put16(f, 16, tl)
+        _put16(f, 24, 0)
+        _put16(f, 24, ipv4_header_sum16(bytes(f[14:34])))
+        ip = bytes(f[14:])
+        if proto == IPPROTO_TCP:
+            _put16(f, la + 16, 0)
+            _put16(f, la + 16, ipv4_tcp_pseudo(ip).payload_sum16(bytes(f[la:])))
+        elif proto == IPPROTO_UDP:
+            c = ipv4_udp_pseudo(ip, n)
+            _put16(f, la + 4, n)
+            _put16(f, la + 6, 0)
+            _put16(f, la + 6, never_zero_sum(c.payload_sum16(bytes(f[la:]))))
+        elif proto == IPPROTO_ICMP:
+            _put16(f, la + 2, 0)
+            _put16(f, la + 2, CRC791().payload_sum16(bytes(f[la:])))
+        return bytes(f), 0
+    if et == ETHERTYPE_IPV6:
+        if len(f) < 54:
+            return bytes(frame), ERR_TRUNCATED_FRAME
+        n, proto = len(f) - 54, f[20]
+        if n > 0xFFFF:
+            return bytes(frame), ERR_INVALID_LENGTH_FIELD
+        need = {IPPROTO_TCP: 20, IPPROTO_UDP: 8, IPPROTO_ICMPV6: 8}.get(proto, 0)
+        if n < need:
+            return bytes(frame), ERR_TRUNCATED_FRAME
+        _put16(f, 18, n)
+        if proto in (IPPROTO_TCP, IPPROTO_UDP, IPPROTO_ICMPV6):
+            c = ipv6_pseudo(bytes(f[14:54]))
+            at = {IPPROTO_TCP: 16, IPPROTO_UDP: 6, IPPROTO_ICMPV6: 2}[proto]
+            if proto == IPPROTO_UDP:
+                _put16(f, 58, n)
+            _put16(f, 54 + at, 0)
+            s = c.payload_sum16(bytes(f[54:]))
+            _put16(f, 54 + at, never_zero_sum(s) if proto == IPPROTO_UDP else s)
+        return bytes(f), 0
+    return bytes(frame), 0
+
+
 # ------------------------------------------------------------ TX FCS append
 ERR_SHORT_BUFFER = 6
 
