@@ -65,6 +65,34 @@ def workload_spec(name: str, world: int):
     raise SystemExit(f"unknown workload {name}")
 
 
+def go_maxprocs() -> tuple[int, str]:
+    """The thread count Go's runtime would default GOMAXPROCS to on this host
+    (go1.25+, the reference's CI runs go1.26): the CPUs this process may run
+    on (sched_getaffinity, what `nproc` prints), capped by a cgroup v2 CPU
+    bandwidth limit when one is set (rounded up, at least 2)."""
+    n = len(os.sched_getaffinity(0))
+    rule = f"sched_getaffinity {n}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            lim = max(2, -(-int(quota) // int(period)))
+            rule += f", cgroup cpu.max {quota}/{period} -> {lim}"
+            n = min(n, lim)
+    except (OSError, ValueError):
+        pass
+    return n, rule
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: int | None = None, op: str = "crc32"):
     """Time the C oracle on a bounded sample of the same frames: for CRC-32 the
     restatement of Go hash/crc32 as its amd64 build runs ethernet/crc.go:19-21
@@ -72,8 +100,9 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
     plain slicing-by-8 form is reported beside it), for --op sum16 the
     crc.go:52-59 restatement."""
     from oracle import oracle as O
+    rule = "given"
     if threads is None:
-        threads = min(16, os.cpu_count() or 1)
+        threads, rule = go_maxprocs()
     if op == "search":
         # the C restatement of ethernet/crc.go:28-47 (crc32.Update per byte), one thread
         nsamp = min(len(off_np) - 1, 256)
@@ -86,6 +115,7 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
             reps += 1
         el = time.perf_counter() - t0
         return {"value": round(reps * sb / el / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                "cpu_model": cpu_model(),
                 "sample": f"{nsamp} captures x {frame_len} B; C restatement of ethernet/crc.go CRC32Search "
                           "(one crc32.Update per byte), NOT lneto's Go binary"}
     if op == "sum16":
@@ -118,6 +148,7 @@ def cpu_baseline(d_bytes, off_np, frame_len, budget_s: float = 10.0, threads: in
         res[(t, fast)] = reps * sample_bytes / el / 2**30
     out = {
         "value": round(res[(threads, amd64)], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model(), "threads_rule": "GOMAXPROCS default: " + rule,
         "value_1core": round(res[(1, amd64)], 3),
         "sample": f"{nsamp} frames x {frame_len or 'zipf'} B ({sample_bytes/1e6:.0f} MB) of the same synthetic batch, "
                   f"repeated for ~{slot:.0f}s per form; " + (
@@ -179,7 +210,8 @@ def main():
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32",
-                    choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search"])
+                    choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search",
+                             "tx_checksum"])
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
@@ -271,15 +303,20 @@ def main():
         fcs = L.crc32_segments(d_bytes, starts, lens)
         fr[:, flen - 4:] = fcs.view(torch.uint8).view(n_local, 4)
         d_hit = torch.empty(n_local, dtype=torch.int64, device=dev)
-    elif args.op == "ingress":
+    elif args.op in ("ingress", "tx_checksum"):
         if flen is None or flen < 42:
-            raise SystemExit("--op ingress needs fixed-size frames of at least 42 bytes")
+            raise SystemExit(f"--op {args.op} needs fixed-size frames of at least 42 bytes")
         fr = d_bytes[: n_local * flen].view(n_local, flen)
         hdr = bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0]) + (flen - 14).to_bytes(2, "big") \
             + bytes.fromhex("12344000401100 00c0a80a01c0a80a02".replace(" ", "")) \
             + bytes.fromhex("14e90035") + (flen - 34).to_bytes(2, "big")
         fr[:, : len(hdr)] = torch.tensor(list(hdr), dtype=torch.uint8, device=dev)
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+        if args.op == "tx_checksum":
+            # TX: the same frames as segments (start, len); the step writes the IPv4
+            # header CRC and the UDP CRC in place, idempotently, every step
+            d_seg = d_off[:-1].contiguous()
+            d_len = (d_off[1:] - d_off[:-1]).to(torch.int32)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -289,6 +326,8 @@ def main():
             L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "ingress":
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+        elif args.op == "tx_checksum":
+            L.tx_checksum_batch(d_bytes, d_seg, d_len, status=d_ok, stream=stream)
         elif args.op == "search":
             L.crc32_search_batch(d_bytes, d_off, out=d_hit, stream=stream)
         elif args.op == "fcs_append":
@@ -352,6 +391,7 @@ def main():
         "ingress": "GiB/s receive-path checksum verdicts (IPv4 header + UDP) over device-resident frames",
         "search": "GiB/s CRC32Search over device-resident captures (bytes scanned to the FCS hit)",
         "fcs_append": "GiB/s TX FCS append (pad, CRC-32, LE32 store) over device-resident ring slots",
+        "tx_checksum": "GiB/s TX checksum generate (IPv4 header + UDP) over device-resident frames",
     }[args.op]
     out = {
         "metric": metric,
@@ -387,7 +427,8 @@ def main():
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
                        "search": "lnx::crc32_search_u_kernel<2>",
-                       "fcs_append": "lnx::crc32_rows_kernel<kCrc> (segment mode) + pad / store"}[args.op],
+                       "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
+                       "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_launches": len(timed),
             "algorithmic_bytes_per_launch": nbytes,
@@ -407,7 +448,7 @@ def main():
         if args.op == "sum16":
             got = d_sum.cpu().numpy().view(np.uint16)
             seeds = d_seed.cpu().numpy().view(np.uint32)
-        elif args.op in ("fcs_verify", "ingress"):
+        elif args.op in ("fcs_verify", "ingress", "tx_checksum"):
             got = d_ok.cpu().numpy()
         elif args.op == "search":
             got = d_hit.cpu().numpy()
@@ -430,6 +471,11 @@ def main():
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
             elif args.op == "ingress":
                 want = O.ingress_verdict(fr)
+            elif args.op == "tx_checksum":
+                # the finished frame is a fixed point of the step and passes the receive path
+                regen, st = O.tx_checksum(fr)
+                assert st == 0 and regen == fr and O.ingress_verdict(fr) == 0, f"frame {i}"
+                want = 0
             elif args.op == "search":
                 want = O.crc32_search(fr, 0)
             else:
@@ -454,7 +500,7 @@ def main():
         out["pcie_inclusive"] = {"value": round(nbytes / el / 2**30, 2), "unit": "GiB/s",
                                  "note": "pinned H2D of frames + kernel + D2H of CRCs, serial, 1 stream"}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op != "fcs_append":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op not in ("fcs_append", "tx_checksum"):
         out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget, op=args.op)
 
     if rank == 0:

@@ -226,6 +226,23 @@ int lnx_rx_ring_ingress(lnx_rx_ring* ring, uint32_t first, uint32_t count, uint3
 int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
                         uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict);
 
+/* netdev.Stack.EgressPackets(bufs, sizes, offset) (x/netdev/interface.go:85;
+ * xnet.Netstack.EgressPackets, x/xnet/netstack.go:87-98) for the device's part
+ * of the transmit path: frame k = bufs[k][offset : offset + lens[k]] is what
+ * the stack wrote (Ethernet header + IP packet, before padding and FCS).  With
+ * LNX_TX_CHECKSUM its length fields and checksums are generated as
+ * lnx_tx_checksum_batch does; with LNX_TX_FCS it is padded to 60 bytes and
+ * its LE FCS appended as lnx_fcs_append_batch does, within `capacity` bytes
+ * (<= the ring's slot_cap).  The frames come back in place, lens[k] = the new
+ * length; status[k] (may be NULL) = the checksum step's status if non-zero,
+ * else the append's (0, or 6 ErrShortBuffer with the frame unpadded).
+ * Synchronous; the batches are pipelined over the ring's stages (gather, H2D,
+ * kernels, D2H, scatter), nothing is retained after the call. */
+#define LNX_TX_CHECKSUM 1u
+#define LNX_TX_FCS 2u
+int lnx_egress_packets(lnx_rx_ring* ring, uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset,
+                       uint32_t capacity, uint32_t flags, uint8_t* status);
+
 /* Number of visible HIP devices (0 when none). */
 int lnx_device_count(void);
 

@@ -84,6 +84,8 @@ _sig = {
                                            _vp, _vp]),
     "lnx_ingress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                            _vp, _vp]),
+    "lnx_egress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
     "lnx_last_error": (ctypes.c_char_p, []),
     "lnx_version": (ctypes.c_char_p, []),
@@ -350,6 +352,7 @@ def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
 
 
 VERIFY_EVIL_BIT = 1  # LNX_VERIFY_EVIL_BIT
+TX_CHECKSUM, TX_FCS = 1, 2  # LNX_TX_CHECKSUM, LNX_TX_FCS
 
 
 def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None):
@@ -475,6 +478,33 @@ class RxRing:
         _check(lib.lnx_ingress_packets(self._h, ptrs, lens.ctypes.data, n, offset, flags, ok.ctypes.data,
                                        verdict.ctypes.data), "lnx_ingress_packets")
         return ok[:n], verdict[:n]
+
+    def egress_packets(self, bufs, sizes, offset: int = 0, capacity: int | None = None,
+                       flags: int = 3):
+        """EgressPackets(bufs, sizes, offset) for the device's part of the transmit
+        path (lnx_egress_packets): bufs are writable uint8 numpy arrays, frame k =
+        bufs[k][offset : offset + sizes[k]]; flags TX_CHECKSUM | TX_FCS.  The frames
+        are finished in place; returns (new sizes, status) as uint32 / uint8 arrays."""
+        import numpy as np
+        n = len(bufs)
+        for b in bufs:
+            if not isinstance(b, np.ndarray) or b.dtype != np.uint8 or not b.flags.c_contiguous \
+                    or not b.flags.writeable:
+                raise LnetoError("egress_packets: bufs must be writable contiguous uint8 numpy arrays")
+        if capacity is None:
+            capacity = self.slot_cap
+        lens = np.ascontiguousarray(np.asarray(sizes, dtype=np.uint32)).copy()
+        if len(lens) != n:
+            raise LnetoError("egress_packets: one size per buffer")
+        for b, l in zip(bufs, lens):  # the finished frame is written back at bufs[k][offset:]
+            if b.size - offset < min(capacity, max(int(l), 60) + 4):
+                raise LnetoError("egress_packets: each buffer needs room for its padded frame and FCS "
+                                 "(min(capacity, max(size, 60) + 4) bytes from offset)")
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[b.ctypes.data for b in bufs])
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        _check(lib.lnx_egress_packets(self._h, ptrs, lens.ctypes.data, n, offset, capacity, flags,
+                                      status.ctypes.data), "lnx_egress_packets")
+        return lens[:n], status[:n]
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -27,8 +27,7 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
-                             uint8_t* status, uint32_t* crc_scratch, const void* images, int num_cus,
-                             hipStream_t stream);
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
@@ -258,14 +257,10 @@ int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  const hipStream_t s = static_cast<hipStream_t>(stream);
-  uint32_t* crc = nullptr;  // stream-ordered scratch for the CRCs
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&crc), n * 4, s);
-  if (e != hipSuccess) return hip_fail(e, "hipMallocAsync(fcs scratch)");
-  e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, crc, c->d_image, c->num_cus, s);
-  const hipError_t f = hipFreeAsync(crc, s);
-  if (e != hipSuccess) return hip_fail(e, "fcs append launch");
-  if (f != hipSuccess) return hip_fail(f, "hipFreeAsync(fcs scratch)");
+  // one launch of the CRC kernel in its append mode: no scratch, no allocation
+  const hipError_t e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, c->d_image, c->num_cus,
+                                         static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel (append) launch");
   return LNX_OK;
 }
 

@@ -324,7 +324,16 @@ __device__ __forceinline__ void slot_wait(Word (&w)[KS], uint32_t& junk, uint32_
   asm volatile("" : "+v"(junk), "+v"(b0), "+v"(b1));
 }
 
-enum class CrcMode : int { kCrc = 0, kVerify = 1 };
+// kAppend (segment mode only): the TX FCS append of lnx_fcs_append_batch
+// (internet/stack-ethernet.go:200-214) — frame i is zero-padded to 60 bytes
+// and LE32(CRC32(padded frame)) is written after it, len[i] = padded + 4,
+// status[i] = 0; a frame whose padded length + 4 exceeds the capacity is left
+// untouched with status 6 (ErrShortBuffer).  The CRC of the padded frame is
+// the frame's register advanced over the k = 60 - n pad bytes (zero_advance):
+// the pad is written, never read.
+enum class CrcMode : int { kCrc = 0, kVerify = 1, kAppend = 2 };
+constexpr uint32_t kMinFrame = 60;
+constexpr uint8_t kErrShortBuffer = 6;
 
 // The result of frame f: its CRC, or (verify mode) 1 if the residue matches.
 template <CrcMode MODE>
@@ -344,13 +353,61 @@ struct Lanes {
   uint32_t lane, p, row, bu0, bu1, bf, bt;
 };
 
+// Z_k(x), k = 1 .. 4 SB (k zero bytes appended to the register x; k = 0:
+// identity), for a row-uniform x and k, with the tables of the image the
+// workgroup loaded (row width IMGRL: U = Z_SB, SB = 4 IMGRL; column c of F is
+// Z_{-4 (c mod IMGRL)}; T = Z_{-t}, t < 4): Z_k = U^m o Z_{-4a} o Z_{-b} with
+// m = ceil(k / SB) and m SB - k = 4a + b.  RL: lanes per row (t_fix's row).
+template <int RL, int IMGRL>
+__device__ __forceinline__ uint32_t zero_advance(const char* lds, uint32_t x, uint32_t k, const Lanes& L) {
+  constexpr uint32_t SB = 4u * IMGRL;
+  const uint32_t m = (k + SB - 1u) / SB, d = m * SB - k;
+  if (wave_any((d >> 2) != 0u)) {
+    const uint32_t c = ((L.lane & 31u) & ~(uint32_t)(IMGRL - 1)) | (d >> 2);
+    const uint32_t y = f_step(lds, x, kFBase | (c << 2));
+    x = (d >> 2) ? y : x;
+  }
+  x = t_fix<RL>(lds, x, d & 3u, L.p, L.bt);
+  for (uint32_t i = 0; wave_any(i < m); ++i) {
+    const uint32_t y = u_step(lds, x, L.bu0, L.bu1);
+    x = i < m ? y : x;
+  }
+  return x;
+}
+
+// The append tail of one frame (row-uniform n, R = its register before the
+// final complement, e = address of its end byte): the k = 60 - n pad bytes and
+// the LE FCS are written by the row's lanes (byte j = j0 + p), lane 0 writes
+// the new length and the status.  live: the row holds a finished frame.
+template <int RL, int IMGRL>
+__device__ __forceinline__ void append_tail(const char* lds, const Lanes& L, bool live, uint32_t n, uint32_t R,
+                                            uint8_t* e, uint32_t cap, uint32_t* len_at, uint8_t* status_at) {
+  const uint32_t k = live && n < kMinFrame ? kMinFrame - n : 0u;
+  if (wave_any(k != 0u)) {
+    const uint32_t z = zero_advance<RL, IMGRL>(lds, R, k, L);
+    R = k ? z : R;
+  }
+  const uint32_t crc = ~R;
+  const uint32_t pl = n + k;
+  const bool ok = live && (uint64_t)pl + 4u <= cap;
+  const uint32_t tot = k + 4u;
+  for (uint32_t j0 = 0; wave_any(ok && j0 < tot); j0 += RL) {
+    const uint32_t j = j0 + L.p;
+    if (ok && j < tot) e[j] = j < k ? (uint8_t)0 : (uint8_t)(crc >> (8u * (j - k)));
+  }
+  if (live && L.p == 0) {
+    if (ok) *len_at = pl + 4u;
+    *status_at = ok ? (uint8_t)0 : kErrShortBuffer;
+  }
+}
+
 // ------------------------------------------------------------------ generic path
 // For a wave whose byte range does not fit a 31-bit buffer offset (frames of
 // gigabytes): same algorithm with the window ending exactly at the frame end,
 // byte loads with explicit bounds, no pipelining.
 template <CrcMode MODE, int RL>
 __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* bytes, const uint64_t* off,
-                             const uint32_t* seg_len, uint64_t fw0, uint64_t fw1, void* out) {
+                             const uint32_t* seg_len, uint64_t fw0, uint64_t fw1, void* out, uint32_t cap) {
   constexpr uint32_t NR = 64 / RL, SB = 4 * RL;
   const uint64_t fend = fw0 + ((fw1 - fw0 + NR - 1) / NR) * NR;
   for (uint64_t f = fw0 + L.row; f < fend; f += NR) {
@@ -375,6 +432,11 @@ __device__ void rows_generic(const char* lds, const Lanes& L, const uint8_t* byt
     }
     uint32_t R = n ? row_xor<RL>(f_step(lds, reg, L.bf)) : 0u;
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    if constexpr (MODE == CrcMode::kAppend) {  // segment mode: n < 2^32
+      append_tail<RL, RL>(lds, L, live, (uint32_t)n, R, const_cast<uint8_t*>(bytes) + e, cap,
+                          const_cast<uint32_t*>(seg_len) + f, reinterpret_cast<uint8_t*>(out) + f);
+      continue;
+    }
     const uint32_t crc = ~R;
     if (live && L.p == 0) {
       if (MODE == CrcMode::kCrc)
@@ -393,6 +455,11 @@ struct WaveCtx {
   uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase)
   __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc;
   __amdgpu_buffer_rsrc_t len_rsrc;  // segment mode: the length array
+  // kAppend: the byte at rel 0, the range's lengths (written back) and status bytes, the slot capacity
+  uint8_t* data_base;
+  uint32_t* lenw;
+  uint8_t* stat;
+  uint32_t cap;
 };
 
 // RL: lanes per row, KS: window steps per item, S: ring slots, CH: frames per
@@ -483,6 +550,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   uint32_t fi[S], sb[S], eb[S];  // lane i: frame of virtual index nfv[s] + i, its start / end (low dwords)
   uint32_t nfv[S];            // uniform
   uint32_t it_f[S], it_n[S], it_t[S], it_j0[S], it_ns[S];
+  uint32_t it_e[S];           // kAppend: rel(end) of the item's frame
   bool hw[S];                 // uniform: slot holds work
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -490,7 +558,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     for (int k = 0; k < KS; ++k) w[s][k] = 0;
     jk[s] = 0;
     it_f[s] = kNoFrame;
-    it_n[s] = it_t[s] = it_j0[s] = it_ns[s] = 0;
+    it_n[s] = it_t[s] = it_j0[s] = it_ns[s] = it_e[s] = 0;
     hw[s] = false;
     nfv[s] = 0;
   }
@@ -570,6 +638,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     it_f[s] = rf;
     it_n[s] = rn;
     it_t[s] = rt;
+    it_e[s] = rea - rt;
     it_j0[s] = rj;
     it_ns[s] = ns;
     hw[s] = wave_any(alive);
@@ -630,7 +699,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   // so its LDS round trips overlap them instead of idling the wave.
   struct Fin {
     uint32_t reg[WL];
-    uint32_t junk, f, n, t;
+    uint32_t junk, f, n, t, e;
     bool last, any;
   };
   auto compute = [&](auto sc) -> Fin {
@@ -731,6 +800,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     fin.f = it_f[s];
     fin.n = n;
     fin.t = t;
+    fin.e = it_e[s];
     fin.last = last;
     fin.any = wave_any(last);
     return fin;
@@ -777,10 +847,16 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
       crc = ~R;
+      if constexpr (MODE == CrcMode::kAppend) {
+        const bool lv = fin.last && fin.f != kNoFrame;
+        append_tail<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.data_base + fin.e, cx.cap, cx.lenw + fin.f,
+                                         cx.stat + fin.f);
+      }
     }
     // hold the result; a flush adds a vmcnt event after the slot's loads,
     // which only makes the waits of rows_body stricter
-    if constexpr (!kHold) {
+    if constexpr (MODE == CrcMode::kAppend) {
+    } else if constexpr (!kHold) {
       store_result<MODE>(out_rsrc, fin.last && p == 0, fin.f, result_of<MODE>(n, crc));
     } else {
       if (fin.last && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
@@ -820,7 +896,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }(std::make_integer_sequence<int, S>{});
   }
 #undef LNX_FENCE
-  if (kHold && wave_any(pc != 0)) flush();
+  if (MODE != CrcMode::kAppend && kHold && wave_any(pc != 0)) flush();
   // drain: no asm load may still be writing registers when the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -888,7 +964,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
 
   // row-uniform parameters of the frame in progress
   struct Rowp {
-    uint32_t f, n, t, J, ws;
+    uint32_t f, n, t, J, ws, e;
   };
   auto setup = [&](uint32_t b, uint32_t bd) -> Rowp {
     Rowp r;
@@ -902,6 +978,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     const uint32_t rs = s - o0_lo + adj, re = e - o0_lo + adj;
     const uint32_t wend = (re + 127u) & ~127u;
     r.ws = rs & ~127u;
+    r.e = re;
     r.t = wend - re;
     r.J = r.n ? (wend - r.ws) >> 7 : 0u;
     return r;
@@ -990,7 +1067,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   };
 
   struct Fin {
-    uint32_t r0, r1, junk, f, n, t;
+    uint32_t r0, r1, junk, f, n, t, e;
   };
   auto fold = [&](const Rowp& r) -> Fin {
     const uint32_t n = r.n, t = r.t, J = r.J, a = t >> 2;
@@ -1111,6 +1188,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     fin.f = r.f;
     fin.n = n;
     fin.t = t;
+    fin.e = r.e;
     return fin;
   };
 
@@ -1148,6 +1226,11 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     }
     R = n != 0 ? R : 0u;
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+    if constexpr (MODE == CrcMode::kAppend) {
+      append_tail<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.data_base + fin.e, cx.cap, cx.lenw + fin.f,
+                                         cx.stat + fin.f);
+      return;
+    }
     const uint32_t crc = ~R;
     if (live && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
     pc += live ? 1u : 0u;
@@ -1195,7 +1278,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   // load is outstanding here, but the explicit wait lets the linear ISA audit
   // (tools/prof/audit_ring.py) see that before the epilogue reuses registers
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (wave_any(pc != 0)) store_result<MODE>(out_rsrc, p < pc, hf, hv);
+  if (MODE != CrcMode::kAppend && wave_any(pc != 0)) store_result<MODE>(out_rsrc, p < pc, hf, hv);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
@@ -1225,7 +1308,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
                   uint64_t* __restrict__ timeline,
-                  const uint32_t* __restrict__ seg_len) {
+                  const uint32_t* __restrict__ seg_len, uint32_t cap) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path
@@ -1331,6 +1414,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
                                                     (int)(cx.nfb * elem), 0x00020000);
     cx.o0_lo = (uint32_t)r.o0;
     cx.ctr = lds_words + kCtrBase / 4;
+    cx.data_base = const_cast<uint8_t*>(bytes + r.o0 - cx.adj);
+    cx.lenw = const_cast<uint32_t*>(SEG ? seg_len + r.f0 : seg_len);
+    cx.stat = reinterpret_cast<uint8_t*>(out) + r.f0;
+    cx.cap = cap;
     return cx;
   };
   const Range own = range_of(blockIdx.x, ob0, ob1);
@@ -1340,13 +1427,13 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
-      rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
+      rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out, cap);
     } else if (!line) {
       L.p = lane & 15u, L.row = lane >> 4;
-      rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
+      rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out, cap);
     } else {  // the RL = 32 image: 32-lane rows
       L.p = lane & 31u, L.row = lane >> 5;
-      rows_generic<MODE, 32>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out);
+      rows_generic<MODE, 32>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out, cap);
     }
   } else {
     // chunks of the own slice from the LDS counter
@@ -1370,9 +1457,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
 }
 
-hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
+hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                        const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr,
-                       const uint32_t* seg_len = nullptr) {
+                       const uint32_t* seg_len = nullptr, uint32_t cap = 0) {
+  const bool verify = mode == CrcMode::kVerify;
   if (n == 0) return hipSuccess;
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
   uint64_t grid = (n + per_block - 1) / per_block;
@@ -1383,12 +1471,14 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
-                     timeline, seg_len)
+                     timeline, seg_len, cap)
   if (seg_len) {  // segment mode (lnx_crc32_segments, the TX FCS append, the receive ring)
     // (every lean-row step non-temporal, EP = 0, was measured no faster for
     // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
     if (verify)
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
+    else if (mode == CrcMode::kAppend)
+      LNX_LAUNCH(CrcMode::kAppend, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else
       LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 12, 2, 4, 16, true);
   } else if (verify) {
@@ -1480,23 +1570,28 @@ hipError_t launch_rows(int var, bool verify, const uint8_t* bytes, const uint64_
 // Host-side launch helpers (called from api.cpp).
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
                                const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, verify, bytes, off, n, out, images, num_cus, stream);
+  return launch_rows(0, verify ? CrcMode::kVerify : CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream);
 }
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
   // 80 / 81: the product with 2 / 4 workgroups per CU over the launch (one is
   // resident at a time: the later ones go to the CUs that finish first)
   if (var == 80 || var == 81)
-    return launch_rows(0, false, bytes, off, n, out, images, num_cus * (var == 80 ? 2 : 4), stream, nullptr);
-  return launch_rows(var, false, bytes, off, n, out, images, num_cus, stream, timeline);
+    return launch_rows(0, CrcMode::kCrc, bytes, off, n, out, images, num_cus * (var == 80 ? 2 : 4), stream, nullptr);
+  return launch_rows(var, CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream, timeline);
 }
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, false, bytes, start, n, out, images, num_cus, stream, nullptr, len);
+  return launch_rows(0, CrcMode::kCrc, bytes, start, n, out, images, num_cus, stream, nullptr, len);
 }
 hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                       uint8_t* ok, const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, true, bytes, start, n, ok, images, num_cus, stream, nullptr, len);
+  return launch_rows(0, CrcMode::kVerify, bytes, start, n, ok, images, num_cus, stream, nullptr, len);
+}
+// TX FCS append in place (kAppend, one launch): pad to 60, LE FCS, len += pad + 4, status.
+hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream) {
+  return launch_rows(0, CrcMode::kAppend, bytes, start, n, status, images, num_cus, stream, nullptr, len, capacity);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

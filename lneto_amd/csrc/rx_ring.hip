@@ -40,6 +40,10 @@ hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* star
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
                                  uint32_t trim);
+hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
+                              uint8_t* status, int num_cus, hipStream_t stream);
+hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream);
 
 // Slot i of the batch: frame = slot[offset : min(len, cap)].
 __global__ void __launch_bounds__(256)
@@ -130,6 +134,53 @@ int sync_all(lnx_rx_ring* r) {
   return rc;
 }
 
+// Transmit direction, slots [b0, b0 + nb) on stage `s` (asynchronous): the
+// frames (slot[0 : len]) get their checksums (LNX_TX_CHECKSUM) and their
+// padding + FCS (LNX_TX_FCS) on the device, and come back whole with their
+// new lengths; h_verdict = the checksum status, h_ok = the append status.
+int enqueue_tx(lnx_rx_ring* r, lnx_rx_ring::Stage& s, uint32_t b0, uint32_t nb, uint32_t capacity, uint32_t flags) {
+  hipError_t e;
+  const size_t cap = r->cap;
+  if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
+                          s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring H2D");
+  const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
+  hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, 0u);
+  if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
+  if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess || (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring status reset");
+  if ((flags & LNX_TX_CHECKSUM) &&
+      (e = launch_tx_checksum(s.d_bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring checksum launch");
+  if ((flags & LNX_TX_FCS) &&
+      (e = launch_fcs_append(s.d_bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
+          hipSuccess)
+    return hip_error(e, "tx ring FCS append launch");
+  if ((e = hipMemcpyAsync(r->h_slots + (size_t)b0 * cap, s.d_bytes, (size_t)nb * cap, hipMemcpyDeviceToHost,
+                          s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->h_len + b0, s.d_len, (size_t)nb * 4, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->h_ok + b0, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(r->h_verdict + b0, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring D2H");
+  return LNX_OK;
+}
+
+// Host copies of a batch, split over up to 16 threads when it is large.
+template <typename F>
+void parallel_for(uint32_t nb, F&& fn) {
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint32_t nth = nb >= 4096 ? hw : 1;
+  if (nth == 1) {
+    fn(0u, nb);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nth; ++t)
+    th.emplace_back(fn, (uint32_t)((uint64_t)nb * t / nth), (uint32_t)((uint64_t)nb * (t + 1) / nth));
+  for (auto& t : th) t.join();
+}
+
 void copy_out(const lnx_rx_ring* r, uint32_t first, uint32_t count, uint8_t* fcs_ok, uint8_t* verdict) {
   if (fcs_ok) std::memcpy(fcs_ok, r->h_ok + first, count);
   if (verdict) std::memcpy(verdict, r->h_verdict + first, count);
@@ -204,6 +255,63 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
   const int rs = sync_all(r);
   if (rc == LNX_OK) rc = rs;
   if (rc == LNX_OK) copy_out(r, first, count, fcs_ok, verdict);
+  return rc;
+}
+
+int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset,
+                       uint32_t capacity, uint32_t flags, uint8_t* status) {
+  if (!r || (n > 0 && (!bufs || !lens))) return LNX_EINVAL;
+  if (capacity > r->cap || (flags & ~(uint32_t)(LNX_TX_CHECKSUM | LNX_TX_FCS)) != 0) return LNX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (lens[i] > capacity || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
+  if (n == 0) return LNX_OK;
+  std::lock_guard<std::mutex> lk(r->mu);
+  hipError_t e = hipSetDevice(r->device);
+  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+  // as lnx_ingress_packets: batches round-robin over the stages, the gather of
+  // batch k + 1 and the scatter of batch k - depth + 1 overlap the device work
+  const uint32_t depth = std::min(r->depth, r->nslots);
+  const uint32_t per = std::min(r->batch, r->nslots / depth);
+  int rc = LNX_OK;
+  std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});
+  auto drain = [&](uint32_t k) {
+    const hipError_t se = hipStreamSynchronize(r->st[k].s);
+    if (se != hipSuccess) return hip_error(se, "tx ring hipStreamSynchronize");
+    const uint64_t f0 = pending[k].first;
+    const uint32_t cnt = pending[k].second, s0 = k * per;
+    parallel_for(cnt, [&](uint32_t a, uint32_t b) {
+      for (uint32_t j = a; j < b; ++j) {
+        const uint32_t l = r->h_len[s0 + j];
+        if (l) std::memcpy(bufs[f0 + j] + offset, r->h_slots + (size_t)(s0 + j) * r->cap, l);
+        lens[f0 + j] = l;
+        if (status) status[f0 + j] = r->h_verdict[s0 + j] ? r->h_verdict[s0 + j] : r->h_ok[s0 + j];
+      }
+    });
+    pending[k].second = 0;
+    return LNX_OK;
+  };
+  uint64_t i0 = 0;
+  for (uint32_t k = 0; i0 < n && rc == LNX_OK; ++k, i0 += per) {
+    const uint32_t sk = k % depth;
+    if (pending[sk].second) rc = drain(sk);
+    if (rc != LNX_OK) break;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
+    const uint32_t s0 = sk * per;
+    parallel_for(nb, [&](uint32_t a, uint32_t b) {
+      for (uint32_t j = a; j < b; ++j) {
+        const uint32_t l = lens[i0 + j];
+        if (l) std::memcpy(r->h_slots + (size_t)(s0 + j) * r->cap, bufs[i0 + j] + offset, l);
+        r->h_len[s0 + j] = l;
+      }
+    });
+    rc = enqueue_tx(r, r->st[sk], s0, nb, capacity, flags);
+    pending[sk] = {i0, nb};
+  }
+  for (uint32_t k = 0; k < depth; ++k) {
+    if (!pending[k].second) continue;
+    const int d = drain(k);
+    if (rc == LNX_OK) rc = d;
+  }
   return rc;
 }
 

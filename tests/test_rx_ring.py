@@ -164,3 +164,41 @@ def test_ingress_packets_fewer_slots_than_stages(cuda, nslots):
     want_ok, want_v = _expect(frames)
     assert np.array_equal(ok, want_ok)
     assert np.array_equal(verdict, want_v)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [L.TX_CHECKSUM | L.TX_FCS, L.TX_FCS, L.TX_CHECKSUM])
+def test_egress_packets_matches_oracle(cuda, flags):
+    """netdev.Stack.EgressPackets(bufs, sizes, offset) (x/netdev/interface.go:85)
+    for the device's part of the transmit path: checksum generate
+    (oracle.tx_checksum), then pad + FCS (oracle.fcs_append), in place in
+    caller-owned buffers, more frames than the ring has slots."""
+    from tests.test_tx_checksum import tx_frames
+    frames = [f for f in tx_frames(seed=60, count=1500) if len(f) <= 2000]
+    offset, cap = 6, 2048
+    rng = np.random.default_rng(61)
+    bufs = []
+    for f in frames:
+        b = rng.integers(0, 256, offset + cap + 16, dtype=np.uint8)
+        b[offset:offset + len(f)] = np.frombuffer(f, dtype=np.uint8)
+        bufs.append(b)
+    before = [b.copy() for b in bufs]
+    ring = L.RxRing(300, slot_cap=cap, batch_slots=128, depth=3)
+    try:
+        sizes, status = ring.egress_packets(bufs, [len(f) for f in frames], offset=offset, capacity=cap,
+                                            flags=flags)
+    finally:
+        ring.close()
+    bad = []
+    for i, f in enumerate(frames):
+        want, st = (O.tx_checksum(f) if flags & L.TX_CHECKSUM else (f, 0))
+        st2 = 0
+        if flags & L.TX_FCS:
+            want, st2 = O.fcs_append(want, cap)
+        got = bufs[i][offset:offset + int(sizes[i])].tobytes()
+        if got != want or int(status[i]) != (st or st2):
+            bad.append((i, len(f), int(sizes[i]), len(want), int(status[i]), st or st2))
+        # bytes outside the finished frame are the caller's
+        assert np.array_equal(bufs[i][:offset], before[i][:offset])
+        assert np.array_equal(bufs[i][offset + len(want):], before[i][offset + len(want):])
+    assert not bad, bad[:10]

@@ -50,6 +50,54 @@ def test_gpu_fcs_append(cuda):
         assert np.array_equal(got[i * CAP + len(want): (i + 1) * CAP], data[i * CAP + len(want): (i + 1) * CAP]), i
 
 
+def _lens(rng, n, cap, shape):
+    """Frame lengths by row layout the CRC kernel's append mode picks from the
+    workgroup's mean: runts only (4-lane rows, up to four U steps of zero
+    advance), ~1500 B (lean line rows), 2-3 KB (one-word 16-lane rows), ~9000 B
+    (32-lane rows); every shape carries runts (k = 1..60 pad bytes) and frames
+    at the capacity edge."""
+    if shape == "runts":
+        lens = rng.integers(0, 61, size=n)
+    elif shape == "mtu":
+        lens = rng.integers(1400, 1515, size=n)
+    elif shape == "mid":
+        lens = rng.integers(1800, 3500, size=n)
+    else:
+        lens = rng.integers(8000, 9100, size=n)
+    lens[5::13] = rng.integers(0, 61, size=len(lens[5::13]))
+    lens[3::17] = cap - rng.integers(0, 8, size=len(lens[3::17]))
+    return np.minimum(lens, cap).astype(np.int64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,cap,base", [("runts", 64, 0), ("runts", 68, 3), ("mtu", 1536, 1), ("mtu", 1536, 0),
+                                            ("mid", 4096, 2), ("jumbo", 9216, 0), ("jumbo", 9220, 3)])
+def test_gpu_fcs_append_layouts(cuda, shape, cap, base):
+    """One launch of the CRC kernel in append mode per batch, every row layout."""
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng([len(shape), cap, base])
+    n = 30000 if shape == "runts" else 6000 if shape in ("mtu", "mid") else 1500
+    lens = _lens(rng, n, cap, shape)
+    data = rng.integers(0, 256, size=base + n * cap + 8, dtype=np.uint8)
+    starts = base + np.arange(n, dtype=np.int64) * cap
+    d = torch.from_numpy(data.copy()).to(cuda)
+    dl = torch.from_numpy(lens.astype(np.int32)).to(cuda)
+    status = L.fcs_append_batch(d, torch.from_numpy(starts).to(cuda), dl, cap).cpu().numpy()
+    got, got_len = d.cpu().numpy(), dl.cpu().numpy()
+    want_img = data.copy()
+    bad = []
+    for i in range(n):
+        s = int(starts[i])
+        want, st = O.fcs_append(data[s:s + int(lens[i])].tobytes(), cap)
+        want_img[s:s + len(want)] = np.frombuffer(want, dtype=np.uint8)
+        if int(status[i]) != st or int(got_len[i]) != len(want):
+            bad.append((i, int(lens[i]), int(status[i]), st, int(got_len[i]), len(want)))
+    assert not bad, bad[:10]
+    diff = np.nonzero(got != want_img)[0]
+    assert diff.size == 0, [(int(x), int((x - base) // cap)) for x in diff[:10]]
+
+
 @pytest.mark.gpu
 def test_gpu_crc32_segments(cuda):
     import torch
