@@ -321,7 +321,16 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       }
       bool first = true;
       uint2 yl = make_uint2(0u, 0u);  // the row's last qword, on the lane that loaded it (outside the first qwords)
-      for (int32_t q0 = qstart + (int32_t)p; q0 < qend; q0 += 16 * UNR) {
+      // A wave-uniform trip count (the most any row of the wave needs): a
+      // loop bounded per row, with dwordx2 loads in it, is the shape that
+      // returned wrong sums in round 1; lanes past their
+      // row's end load nothing (q < qend) and add zeros.
+      int32_t nit = qend > qstart ? (qend - qstart + 16 * UNR - 1) / (16 * UNR) : 0;
+      nit = max(nit, __shfl_xor(nit, 16));
+      nit = max(nit, __shfl_xor(nit, 32));
+      nit = __builtin_amdgcn_readfirstlane(nit);
+      for (int32_t it = 0; it < nit; ++it) {
+        const int32_t q0 = qstart + (int32_t)p + 16 * UNR * it;
         if (!first) {
 #pragma unroll
           for (int u = 0; u < UNR; ++u) {

@@ -32,3 +32,19 @@ def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_ring.py"),
                             str(tmp_path / asm), sym], capture_output=True, text=True)
         assert r.returncode == 0, f"{sym}:\n{r.stdout}"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+@pytest.mark.parametrize("src", ["crc32_kernel", "sum16_kernel", "ingress_kernel", "search_kernel", "rx_ring"])
+def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src):
+    """tools/prof/audit_loops.py over every product kernel: no innermost loop
+    that retires lanes with s_andn2_b64 exec and issues multi-dword loads (the
+    shape of round 1's wrong-sum sum16 form)."""
+    path = os.path.join(ROOT, "lneto_amd", "csrc", src + ".hip")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-mllvm",
+                    "-amdgpu-atomic-optimizer-strategy=None", "-c", "--save-temps", "-o", str(tmp_path / "k.o"), path],
+                   cwd=tmp_path, check=True, capture_output=True)
+    asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_loops.py"), str(tmp_path / asm)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout

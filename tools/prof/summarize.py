@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a tools/prof/profile.sh run into profiles/ (committed evidence).
 
-usage: summarize.py gpurun_out/prof_TAG_WL  profiles/  TAG  WL
+usage: summarize.py gpurun_out/prof_TAG_WL  profiles/  TAG  WL  [KERNEL-SUBSTRING]
 Writes  profiles/TAG_WL_kernel_stats.csv   (rocprofv3 --stats, verbatim)
         profiles/TAG_WL_summary.json       (per-launch averages of every counter)
         profiles/traffic_WL.json           (HBM bytes per launch, calibrated; read by bench.py)
@@ -28,6 +28,9 @@ def per_dispatch(path, match):
 
 def main():
     src, dst, tag, wl = sys.argv[1:5]
+    global KERNEL
+    if len(sys.argv) > 5:
+        KERNEL = sys.argv[5]
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(src, "trace", "trace_kernel_stats.csv")
     shutil.copy(stats, os.path.join(dst, f"{tag}_{wl}_kernel_stats.csv"))
