@@ -338,7 +338,7 @@ constexpr uint8_t kErrShortBuffer = 6;
 // The result of frame f: its CRC, or (verify mode) 1 if the residue matches.
 template <CrcMode MODE>
 __device__ __forceinline__ uint32_t result_of(uint32_t n, uint32_t crc) {
-  return MODE == CrcMode::kCrc ? crc : ((n >= 4 && crc == 0x2144DF1Cu) ? 1u : 0u);
+  return MODE != CrcMode::kVerify ? crc : ((n >= 4 && crc == 0x2144DF1Cu) ? 1u : 0u);
 }
 template <CrcMode MODE>
 __device__ __forceinline__ void store_result(__amdgpu_buffer_rsrc_t out_rsrc, bool st, uint32_t f, uint32_t v) {
@@ -351,6 +351,15 @@ __device__ __forceinline__ void store_result(__amdgpu_buffer_rsrc_t out_rsrc, bo
 // Per-lane constants.
 struct Lanes {
   uint32_t lane, p, row, bu0, bu1, bf, bt;
+};
+
+// kAppend: the byte at rel 0 of the range, its lengths (written back) and
+// status bytes, and the slot capacity.
+struct WaveCtxAppend {
+  uint8_t* data_base;
+  uint32_t* lenw;
+  uint8_t* stat;
+  uint32_t cap;
 };
 
 // Z_k(x), k = 1 .. 4 SB (k zero bytes appended to the register x; k = 0:
@@ -379,6 +388,36 @@ __device__ __forceinline__ uint32_t zero_advance(const char* lds, uint32_t x, ui
 // final complement, e = address of its end byte): the k = 60 - n pad bytes and
 // the LE FCS are written by the row's lanes (byte j = j0 + p), lane 0 writes
 // the new length and the status.  live: the row holds a finished frame.
+// The pad half of append_tail for the pipelined bodies: R advanced over the
+// k = 60 - n pad bytes, which the row's lanes write at e (rare: runts only);
+// the FCS, length and status are held and flushed with the other results
+// (store_held), so the ring's vmcnt waits do not wait on a store per slot.
+template <int RL, int IMGRL>
+__device__ __forceinline__ uint32_t append_pad(const char* lds, const Lanes& L, bool live, uint32_t n, uint32_t R,
+                                               uint8_t* e, uint32_t& k) {
+  k = live && n < kMinFrame ? kMinFrame - n : 0u;
+  if (wave_any(k != 0u)) {
+    const uint32_t z = zero_advance<RL, IMGRL>(lds, R, k, L);
+    R = k ? z : R;
+    for (uint32_t j0 = 0; wave_any(j0 < k); j0 += RL) {
+      const uint32_t j = j0 + L.p;
+      if (j < k) e[j] = 0;
+    }
+  }
+  return R;
+}
+// Held append results of a lane: frame hf (relative), FCS hv at rel position
+// he, new length hpl (0: the frame did not fit, status ErrShortBuffer).
+__device__ __forceinline__ void store_held(const WaveCtxAppend& a, bool st, uint32_t hf, uint32_t hv, uint32_t he,
+                                           uint32_t hpl) {
+  if (st && hpl) {
+    uint8_t* q = a.data_base + he;
+    q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
+    a.lenw[hf] = hpl;
+  }
+  if (st) a.stat[hf] = hpl ? (uint8_t)0 : kErrShortBuffer;
+}
+
 template <int RL, int IMGRL>
 __device__ __forceinline__ void append_tail(const char* lds, const Lanes& L, bool live, uint32_t n, uint32_t R,
                                             uint8_t* e, uint32_t cap, uint32_t* len_at, uint8_t* status_at) {
@@ -455,11 +494,7 @@ struct WaveCtx {
   uint32_t* ctr;             // LDS frame-chunk counter (lds_layout.hpp kCtrBase)
   __amdgpu_buffer_rsrc_t data_rsrc, off_rsrc, out_rsrc;
   __amdgpu_buffer_rsrc_t len_rsrc;  // segment mode: the length array
-  // kAppend: the byte at rel 0, the range's lengths (written back) and status bytes, the slot capacity
-  uint8_t* data_base;
-  uint32_t* lenw;
-  uint8_t* stat;
-  uint32_t cap;
+  WaveCtxAppend ap;                 // kAppend
 };
 
 // RL: lanes per row, KS: window steps per item, S: ring slots, CH: frames per
@@ -595,9 +630,13 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   constexpr bool kWinFlush = kHold && (RL >= 16 || VAR == 5);
   constexpr int kWinLog = 12;
   uint32_t hf = 0, hv = 0, pc = 0;
+  uint32_t he = 0, hpl = 0;  // kAppend: FCS position and new length of the held frame
   uint32_t win = kWinFlush ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog) : 0u;
   auto flush = [&]() {
-    store_result<MODE>(out_rsrc, p < pc, hf, hv);
+    if constexpr (MODE == CrcMode::kAppend)
+      store_held(cx.ap, p < pc, hf, hv, he, hpl);
+    else
+      store_result<MODE>(out_rsrc, p < pc, hf, hv);
     pc = 0;
   };
 
@@ -806,7 +845,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     return fin;
   };
   auto finish = [&](const Fin& fin) {
-    uint32_t crc = 0;
+    uint32_t crc = 0, kpad = 0;
     const uint32_t n = fin.n, t = fin.t;
     if (fin.any) {
       // the lane holding the frame end absorbed t & 3 junk bytes past it: take
@@ -846,20 +885,23 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       }
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
+      if constexpr (MODE == CrcMode::kAppend)
+        R = append_pad<RL, kLine ? 32 : RL>(lds, L, fin.last && fin.f != kNoFrame, n, R, cx.ap.data_base + fin.e,
+                                            kpad);
       crc = ~R;
-      if constexpr (MODE == CrcMode::kAppend) {
-        const bool lv = fin.last && fin.f != kNoFrame;
-        append_tail<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.data_base + fin.e, cx.cap, cx.lenw + fin.f,
-                                         cx.stat + fin.f);
-      }
     }
     // hold the result; a flush adds a vmcnt event after the slot's loads,
     // which only makes the waits of rows_body stricter
-    if constexpr (MODE == CrcMode::kAppend) {
-    } else if constexpr (!kHold) {
+    if constexpr (!kHold) {
       store_result<MODE>(out_rsrc, fin.last && p == 0, fin.f, result_of<MODE>(n, crc));
     } else {
-      if (fin.last && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
+      if (fin.last && p == pc) {
+        hf = fin.f, hv = result_of<MODE>(n, crc);
+        if constexpr (MODE == CrcMode::kAppend) {
+          he = fin.e + kpad;
+          hpl = (uint64_t)n + kpad + 4u <= cx.ap.cap ? n + kpad + 4u : 0u;
+        }
+      }
       pc += fin.last ? 1u : 0u;
       bool fl = wave_any(pc == (uint32_t)RL);
       if constexpr (kWinFlush) {
@@ -896,7 +938,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }(std::make_integer_sequence<int, S>{});
   }
 #undef LNX_FENCE
-  if (MODE != CrcMode::kAppend && kHold && wave_any(pc != 0)) flush();
+  if (kHold && wave_any(pc != 0)) flush();
   // drain: no asm load may still be writing registers when the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
@@ -1195,6 +1237,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   // results held in registers, flushed in clock windows (as rows_body)
   constexpr int kWinLog = 12;
   uint32_t hf = 0, hv = 0, pc = 0;
+  uint32_t he = 0, hpl = 0;  // kAppend (store_held)
   uint32_t win = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
   auto finish = [&](const Fin& fin) {
     const uint32_t n = fin.n, t = fin.t, a = t >> 2;
@@ -1226,20 +1269,27 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     }
     R = n != 0 ? R : 0u;
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
-    if constexpr (MODE == CrcMode::kAppend) {
-      append_tail<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.data_base + fin.e, cx.cap, cx.lenw + fin.f,
-                                         cx.stat + fin.f);
-      return;
-    }
+    uint32_t kpad = 0;
+    if constexpr (MODE == CrcMode::kAppend)
+      R = append_pad<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, kpad);
     const uint32_t crc = ~R;
-    if (live && p == pc) hf = fin.f, hv = result_of<MODE>(n, crc);
+    if (live && p == pc) {
+      hf = fin.f, hv = result_of<MODE>(n, crc);
+      if constexpr (MODE == CrcMode::kAppend) {
+        he = fin.e + kpad;
+        hpl = (uint64_t)n + kpad + 4u <= cx.ap.cap ? n + kpad + 4u : 0u;
+      }
+    }
     pc += live ? 1u : 0u;
     bool fl = wave_any(pc == RL);
     const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog);
     fl = fl || (now != win && wave_any(pc != 0));
     win = now;
     if (fl) {
-      store_result<MODE>(out_rsrc, p < pc, hf, hv);
+      if constexpr (MODE == CrcMode::kAppend)
+        store_held(cx.ap, p < pc, hf, hv, he, hpl);
+      else
+        store_result<MODE>(out_rsrc, p < pc, hf, hv);
       pc = 0;
     }
   };
@@ -1278,7 +1328,12 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   // load is outstanding here, but the explicit wait lets the linear ISA audit
   // (tools/prof/audit_ring.py) see that before the epilogue reuses registers
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (MODE != CrcMode::kAppend && wave_any(pc != 0)) store_result<MODE>(out_rsrc, p < pc, hf, hv);
+  if (wave_any(pc != 0)) {
+    if constexpr (MODE == CrcMode::kAppend)
+      store_held(cx.ap, p < pc, hf, hv, he, hpl);
+    else
+      store_result<MODE>(out_rsrc, p < pc, hf, hv);
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
@@ -1414,10 +1469,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
                                                     (int)(cx.nfb * elem), 0x00020000);
     cx.o0_lo = (uint32_t)r.o0;
     cx.ctr = lds_words + kCtrBase / 4;
-    cx.data_base = const_cast<uint8_t*>(bytes + r.o0 - cx.adj);
-    cx.lenw = const_cast<uint32_t*>(SEG ? seg_len + r.f0 : seg_len);
-    cx.stat = reinterpret_cast<uint8_t*>(out) + r.f0;
-    cx.cap = cap;
+    cx.ap.data_base = const_cast<uint8_t*>(bytes + r.o0 - cx.adj);
+    cx.ap.lenw = const_cast<uint32_t*>(SEG ? seg_len + r.f0 : seg_len);
+    cx.ap.stat = reinterpret_cast<uint8_t*>(out) + r.f0;
+    cx.ap.cap = cap;
     return cx;
   };
   const Range own = range_of(blockIdx.x, ob0, ob1);

@@ -158,9 +158,13 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     bool hdr_sum = false, l4_sum = false;
     int32_t pa = 0, pb = 0, la = 0, lb = 0;  // pseudo-address bytes [pa, pb), transport [la, lb)
     uint32_t lseed = 0;                       // length + protocol words of the pseudo-header
+    // A 16-bit big-endian field value v at an even frame offset adds cv(v) to
+    // the qword rows' little-endian half-word sum S (see the sums below): its
+    // high byte sits at address parity mis & 1
+    auto cv = [&](uint32_t v) -> uint32_t { return (mis & 1u) ? v : (((v & 0xFFu) << 8) | (v >> 8)); };
     // GEN: the fields the step writes (frame offset, new value; 0 = none)
     uint32_t g_off[4] = {0, 0, 0, 0}, g_val[4] = {0, 0, 0, 0};
-    uint32_t g_fix_h = 0, g_fix_t = 0;  // new - old of the summed fields (header, transport), mod 2^32
+    uint32_t g_fix_h = 0, g_fix_t = 0;  // cv(new) - cv(old) of the summed fields (header, transport), mod 2^32
     bool g_nz = false;                   // UDP: NeverZeroSum (crc.go:65-71)
     if constexpr (GEN) {
       if (L < 14) {
@@ -181,17 +185,17 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               hdr_sum = true;
               g_off[0] = 16, g_val[0] = tl;   // SetTotalLength(n + hl)
               g_off[1] = 24;                  // SetCRC(CalculateHeaderCRC()), value after the sums
-              g_fix_h = tl - be(H1, 0) - field16(24);
+              g_fix_h = cv(tl) - cv(be(H1, 0)) - cv(field16(24));
               if (need) {
                 l4_sum = true;
                 la = 14 + hl, lb = L;
                 const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
                 g_off[2] = la + at;
-                g_fix_t = 0u - field16(la + at);
+                g_fix_t = 0u - cv(field16(la + at));
                 if (proto != 1) pa = 26, pb = 34, lseed = nn + proto;  // CRCWriteTCPPseudo / CRCWriteUDPPseudo(n)
                 if (proto == 17) {
                   g_off[3] = la + 4, g_val[3] = nn;  // SetLength(n)
-                  g_fix_t += nn - field16(la + 4);
+                  g_fix_t += cv(nn) - cv(field16(la + 4));
                   g_nz = true;
                 }
               }
@@ -211,10 +215,10 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
               lseed = nn + proto;
               const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
               g_off[2] = 54 + at;
-              g_fix_t = 0u - field16(54 + at);
+              g_fix_t = 0u - cv(field16(54 + at));
               if (proto == 17) {
                 g_off[3] = 58, g_val[3] = nn;
-                g_fix_t += nn - field16(58);
+                g_fix_t += cv(nn) - cv(field16(58));
                 g_nz = true;
               }
             }
@@ -294,6 +298,20 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     // ---- the sums: the first batch is in x; later batches while the summed
     // range [14, end) goes on (kIngUnroll dwords per lane in flight)
     uint32_t hE = 0, hO = 0, tE = 0, tO = 0;
+    // qword rows: S = the sum of the little-endian 16-bit halves of the
+    // aligned dwords, one v_dot2_u32_u16 per dword (the dword rows keep the
+    // even / odd byte sums E, O of two v_dot4 per dword).  S = Σ bytes at even
+    // addresses + 256 Σ bytes at odd addresses; with the frame starting at an
+    // odd address that is 256 E + O itself, at an even one E + 256 O, which is
+    // 256 E + O times 256 modulo 65535 (a byte rotation of the folded sum).
+    // The sums of a frame under 64 KiB never wrap 2^32, so sum16 of the
+    // rotated fold equals sum16 of 256 E + O (RFC 1071 §2(B)).
+    uint32_t hS = 0, tS = 0;
+    auto dot2 = [](uint32_t w, uint32_t acc) -> uint32_t {
+      typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+      const u16x2 ones = {1, 1};
+      return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), ones, acc, false);
+    };
     const bool any_sum = hdr_sum || l4_sum;
     const int32_t end = l4_sum ? lb : (hdr_sum ? 34 : 0);
     const int32_t kend = any_sum ? (end + (int32_t)mis + 3) >> 2 : 0;
@@ -347,18 +365,15 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
             if (u == 0 && first) {
               const uint32_t xh = w & range_mask(o0, ha, hb);
               const uint32_t xt = w & (range_mask(o0, pa, pb) | range_mask(o0, la, lb));
-              hE = __builtin_amdgcn_udot4(xh, wE, hE, false);
-              hO = __builtin_amdgcn_udot4(xh, wO, hO, false);
-              tE = __builtin_amdgcn_udot4(xt, wE, tE, false);
-              tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
+              hS = dot2(xh, hS);
+              tS = dot2(xt, tS);
             } else {
               // summed whole: every qword here lies below qend (later batches
               // load under q < qend; the first batch's qwords at or past qend
               // were zeroed above), so only qword qend - 1 can hold bytes at
               // or past lb; the lane holding it keeps it and takes those bytes
               // back out after the loop
-              tE = __builtin_amdgcn_udot4(w, wE, tE, false);
-              tO = __builtin_amdgcn_udot4(w, wO, tO, false);
+              tS = dot2(w, tS);
             }
           }
         }
@@ -373,8 +388,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       // bytes at or past lb of the last qword (zero unless this lane kept it)
       const int32_t ol = 8 * (qend - 1) - (int32_t)mis;  // frame offset of its first byte
       const uint32_t j0 = yl.x & ing_keep_from(lb - ol), j1 = yl.y & ing_keep_from(lb - ol - 4);
-      tE -= __builtin_amdgcn_udot4(j0, wE, __builtin_amdgcn_udot4(j1, wE, 0u, false), false);
-      tO -= __builtin_amdgcn_udot4(j0, wO, __builtin_amdgcn_udot4(j1, wO, 0u, false), false);
+      tS -= dot2(j0, dot2(j1, 0u));
     }
     for (int32_t k0 = kstart + (int32_t)p; !QW && k0 < kend; k0 += 16 * UNR) {
       if (k0 != kstart + (int32_t)p) {
@@ -395,10 +409,26 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
         tO = __builtin_amdgcn_udot4(xt, wO, tO, false);
       }
     }
-    hE = row_add(hE), hO = row_add(hO), tE = row_add(tE), tO = row_add(tO);
+    // hX, tX: 256 E + O of the header and transport bytes, or (qword rows) a
+    // value congruent to it modulo 65535 that is zero exactly when it is
+    uint32_t hX, tX;
+    if constexpr (QW) {
+      // GEN: the field fixes are row-uniform, added on lane 0 of the row only
+      hS = row_add(hS + (p == 0 ? g_fix_h : 0u)), tS = row_add(tS + (p == 0 ? g_fix_t : 0u));
+      auto conv = [&](uint32_t S) -> uint32_t {
+        if (mis & 1u) return S;
+        uint32_t f = (S & 0xFFFFu) + (S >> 16);
+        f = (f & 0xFFFFu) + (f >> 16);
+        return ((f << 8) | (f >> 8)) & 0xFFFFu;
+      };
+      hX = conv(hS), tX = conv(tS);
+    } else {
+      hE = row_add(hE), hO = row_add(hO), tE = row_add(tE), tO = row_add(tO);
+      hX = 256u * hE + hO, tX = 256u * tE + tO;
+    }
     if constexpr (GEN) {
-      g_val[1] = ing_sum16(256u * hE + hO + g_fix_h);
-      const uint32_t tc = ing_sum16(256u * tE + tO + lseed + g_fix_t);
+      g_val[1] = ing_sum16(hX);
+      const uint32_t tc = ing_sum16(tX + lseed);
       g_val[2] = g_nz && tc == 0 ? 0xFFFFu : tc;
       // lane p stores byte p & 1 (big-endian) of field p >> 1
       const uint32_t k = p >> 1;
@@ -407,9 +437,9 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       if (live && v == 0 && k < 4 && fo != 0)
         const_cast<uint8_t*>(fr)[fo + (p & 1u)] = (uint8_t)((p & 1u) ? fv : fv >> 8);
     } else {
-      if (v == 0 && hdr_sum && ing_sum16(256u * hE + hO) != 0) v = kErrBadCRC;
+      if (v == 0 && hdr_sum && ing_sum16(hX) != 0) v = kErrBadCRC;
       if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
-      if (v == 0 && l4_sum && ing_sum16(256u * tE + tO + lseed) != 0) v = kErrBadCRC;
+      if (v == 0 && l4_sum && ing_sum16(tX + lseed) != 0) v = kErrBadCRC;
     }
     if (live && p == 0) verdict[f] = (uint8_t)v;
   }
