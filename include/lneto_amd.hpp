@@ -180,6 +180,15 @@ inline int AppendFCSBatch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d
   return lnx_fcs_append_batch(d_bytes, d_start, d_len, n, capacity, d_status, stream);
 }
 
+// The checksum step of encapsulate4 / encapsulate6 and the ICMP clients
+// (internet/stack-ip4.go:202-228, internet/stack-ip6.go:167-181) for every
+// frame in ring slots: IPv4 total length / IPv6 payload length, IPv4 header
+// CRC, TCP / UDP (NeverZeroSum) / ICMP CRCs, in place; status 0, 18 or 15.
+inline int GenerateChecksumsBatch(uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
+                                  uint8_t* d_status, void* stream = nullptr) {
+  return lnx_tx_checksum_batch(d_bytes, d_start, d_len, n, d_status, stream);
+}
+
 // Receive-path checksum verdicts of every Ethernet frame (0 or the lneto
 // errGeneric code), StackEthernet.Demux -> demux4 / demux6.
 inline int VerifyIngressBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_verdict,
@@ -218,6 +227,15 @@ class RxRing {
   int IngressPackets(const uint8_t* const* bufs, const uint32_t* lens, uint64_t n, uint32_t offset, uint8_t* fcsOK,
                      uint8_t* verdict, bool evilBit = false) {
     return lnx_ingress_packets(r_, bufs, lens, n, offset, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, fcsOK, verdict);
+  }
+  // netdev.Stack.EgressPackets(bufs, sizes, offset) (x/netdev/interface.go:85)
+  // for the device's part of the transmit path: frame k = bufs[k][offset :
+  // offset + lens[k]] gets its checksums (checksum) and its padding + FCS
+  // (fcs) in place; lens[k] is updated, status[k] = 0, 18, 15 or 6.
+  int EgressPackets(uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset, uint32_t capacity,
+                    uint8_t* status, bool checksum = true, bool fcs = true) {
+    return lnx_egress_packets(r_, bufs, lens, n, offset, capacity,
+                              (checksum ? LNX_TX_CHECKSUM : 0u) | (fcs ? LNX_TX_FCS : 0u), status);
   }
   uint32_t Slots() const { return nslots_; }
   uint32_t SlotCap() const { return cap_; }

@@ -127,6 +127,25 @@ static void TestRxRing() {
   uint8_t ok[2] = {9, 9}, verdict[2];
   EXPECT(ring.Ingress(0, 2, 0, ok, verdict) == LNX_OK, "ingress");
   EXPECT(ok[0] == 1 && ok[1] == 0, "fcs ok %d %d", ok[0], ok[1]);
+  // transmit: an IPv4/UDP frame with stale length and checksum fields, 52 bytes
+  std::vector<uint8_t> buf(2 + 128, 0xEE);
+  uint8_t* e = buf.data() + 2;
+  const uint8_t hdr[] = {0xc0, 0xff, 0xee, 0, 0xde, 0xad, 0x4e, 0x8b, 0x3a, 0xf9, 0xfb, 0x6b, 0x08, 0x00,
+                         0x45, 0, 0x12, 0x34, 0, 1, 0x40, 0, 64, 17, 0xAB, 0xCD, 192, 168, 10, 1, 192, 168, 10, 2,
+                         0x14, 0xe9, 0, 53, 0x77, 0x77, 0x55, 0x55};
+  std::memcpy(e, hdr, sizeof(hdr));
+  for (int i = 0; i < 10; ++i) e[42 + i] = uint8_t('a' + i);
+  uint8_t* bufs[1] = {buf.data()};
+  uint32_t lens[1] = {52};
+  uint8_t st[1] = {9};
+  EXPECT(ring.EgressPackets(bufs, lens, 1, 2, 256, st) == LNX_OK, "egress");
+  EXPECT(st[0] == 0 && lens[0] == 64, "egress status %d len %u", st[0], lens[0]);
+  EXPECT(ethernet::CRC32(lneto::Bytes(e, lens[0])) == LNX_CRC32_RESIDUE, "egress FCS residue");
+  EXPECT(ipv4::CalculateHeaderCRC(lneto::Bytes(e + 14, 20)) == 0, "egress IPv4 header CRC verifies");
+  lneto::CRC791 c;
+  ipv4::CRCWriteUDPPseudo(lneto::Bytes(e + 14, 20), c, 18);
+  EXPECT(c.PayloadSum16(lneto::Bytes(e + 34, 18)) == 0, "egress UDP CRC verifies");
+  EXPECT(buf[0] == 0xEE && buf[1] == 0xEE && buf[2 + 64] == 0xEE, "bytes outside the frame untouched");
 }
 
 int main() {
