@@ -27,7 +27,7 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
-                             uint8_t* status, const void* images, int num_cus, hipStream_t stream);
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
@@ -372,6 +372,21 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                       static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
+  return LNX_OK;
+}
+
+// Profiling hook: TX FCS append variants (0 = the product, results held and
+// flushed; 4 = FCS, length and status stored as each frame finishes).
+int lnx__fcs_append_variant(int var, uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n,
+                            uint32_t capacity, uint8_t* d_status, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_start || !d_len || !d_status) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  const hipError_t e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, c->d_image, c->num_cus,
+                                         static_cast<hipStream_t>(stream), var);
+  if (e != hipSuccess) return hip_fail(e, "fcs append variant launch");
   return LNX_OK;
 }
 

@@ -885,15 +885,21 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       }
       R = n != 0 ? R : 0u;
       if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
-      if constexpr (MODE == CrcMode::kAppend)
-        R = append_pad<RL, kLine ? 32 : RL>(lds, L, fin.last && fin.f != kNoFrame, n, R, cx.ap.data_base + fin.e,
-                                            kpad);
+      if constexpr (MODE == CrcMode::kAppend) {
+        const bool lv = fin.last && fin.f != kNoFrame;
+        if constexpr (kHold)
+          R = append_pad<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.ap.data_base + fin.e, kpad);
+        else  // VAR 4: the FCS, length and status stored at once (A/B)
+          append_tail<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.ap.data_base + fin.e, cx.ap.cap, cx.ap.lenw + fin.f,
+                                           cx.ap.stat + fin.f);
+      }
       crc = ~R;
     }
     // hold the result; a flush adds a vmcnt event after the slot's loads,
     // which only makes the waits of rows_body stricter
     if constexpr (!kHold) {
-      store_result<MODE>(out_rsrc, fin.last && p == 0, fin.f, result_of<MODE>(n, crc));
+      if constexpr (MODE != CrcMode::kAppend)
+        store_result<MODE>(out_rsrc, fin.last && p == 0, fin.f, result_of<MODE>(n, crc));
     } else {
       if (fin.last && p == pc) {
         hf = fin.f, hv = result_of<MODE>(n, crc);
@@ -1270,8 +1276,13 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     R = n != 0 ? R : 0u;
     if (n < 4) R ^= (uint32_t)(0xFFFFFFFFull >> (8 * n));
     uint32_t kpad = 0;
-    if constexpr (MODE == CrcMode::kAppend)
+    if constexpr (MODE == CrcMode::kAppend && VAR == 4) {  // the FCS, length and status stored at once (A/B)
+      append_tail<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, cx.ap.cap, cx.ap.lenw + fin.f,
+                                         cx.ap.stat + fin.f);
+      return;
+    } else if constexpr (MODE == CrcMode::kAppend) {
       R = append_pad<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, kpad);
+    }
     const uint32_t crc = ~R;
     if (live && p == pc) {
       hf = fin.f, hv = result_of<MODE>(n, crc);
@@ -1532,6 +1543,8 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
     // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
     if (verify)
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
+    else if (mode == CrcMode::kAppend && var == 4)  // profiling: FCS stored at once, no hold
+      LNX_LAUNCH(CrcMode::kAppend, 4, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend)
       LNX_LAUNCH(CrcMode::kAppend, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else
@@ -1645,8 +1658,8 @@ hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* star
 }
 // TX FCS append in place (kAppend, one launch): pad to 60, LE FCS, len += pad + 4, status.
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
-                             uint8_t* status, const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, CrcMode::kAppend, bytes, start, n, status, images, num_cus, stream, nullptr, len, capacity);
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var) {
+  return launch_rows(var, CrcMode::kAppend, bytes, start, n, status, images, num_cus, stream, nullptr, len, capacity);
 }
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

@@ -43,7 +43,7 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
-                             uint8_t* status, const void* images, int num_cus, hipStream_t stream);
+                             uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 
 // Slot i of the batch: frame = slot[offset : min(len, cap)].
 __global__ void __launch_bounds__(256)
