@@ -314,6 +314,45 @@ __device__ __forceinline__ void ld_item(uint64_t* w, uint32_t v, __amdgpu_buffer
   }
 }
 
+// The same with dwordx4 loads (four words per lane: 4-lane rows reading 64
+// contiguous bytes per row instruction, the narrow rows of the Zipf mix).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define LNX_L(k) "buffer_load_dwordx4 %[o" #k "], %[v], %[r], 0 offen offset:%[i" #k "]\n\t"
+#define LNX_O(k) [o##k] "=&v"(o[k])
+#define LNX_I(k) [i##k] "i"(IMM0 + (k) * D)
+template <int IMM0, int N, int D>
+__device__ __forceinline__ void ld_run4(u32x4* o, uint32_t v, __amdgpu_buffer_rsrc_t rsrc) {
+  static_assert(N >= 1 && N <= 4 && IMM0 + (N - 1) * D <= 4095, "run shape");
+  if constexpr (N == 4) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2) LNX_L(3)
+                 : LNX_O(0), LNX_O(1), LNX_O(2), LNX_O(3)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2), LNX_I(3));
+  } else if constexpr (N == 3) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1) LNX_L(2)
+                 : LNX_O(0), LNX_O(1), LNX_O(2)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1), LNX_I(2));
+  } else if constexpr (N == 2) {
+    asm volatile("s_nop 4\n\t" LNX_L(0) LNX_L(1)
+                 : LNX_O(0), LNX_O(1)
+                 : [v] "v"(v), [r] "s"(rsrc), LNX_I(0), LNX_I(1));
+  } else {
+    asm volatile("s_nop 4\n\t" LNX_L(0) : LNX_O(0) : [v] "v"(v), [r] "s"(rsrc), LNX_I(0));
+  }
+}
+#undef LNX_L
+#undef LNX_O
+#undef LNX_I
+// Runs of R dwordx4 step loads whose base is out of range (no traffic) unless
+// the item has the run's first step (as ld_item_ns).
+template <int K0, int KS, int D, int R>
+__device__ __forceinline__ void ld_item4_ns(u32x4* w, uint32_t v, uint32_t ns, __amdgpu_buffer_rsrc_t rsrc) {
+  if constexpr (K0 < KS) {
+    constexpr int N = KS - K0 < R ? KS - K0 : R;
+    ld_run4<K0 * D, N, D>(w + K0, (uint32_t)K0 < ns ? v : kOOB, rsrc);
+    ld_item4_ns<K0 + N, KS, D, R>(w, v, ns, rsrc);
+  }
+}
+
 // vmcnt wait naming every register of one slot: the wait, then empty asm
 // statements that "redefine" each register, so no use is scheduled above it.
 template <int N, int KS, typename Word>
@@ -521,10 +560,17 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   constexpr uint32_t NR = 64 / RL;  // rows (frames in flight) per wave
   constexpr uint32_t VL = RL * WL;  // virtual lanes per row
   constexpr uint32_t SB = 4 * VL;   // bytes a row consumes per step
-  constexpr uint32_t kSbLog = VL == 32 ? 7 : VL == 16 ? 6 : 4;
+  constexpr uint32_t kSbLog = VL == 32 ? 7 : VL == 16 ? 6 : 4;  // (4 x 4 words: VL 16)
   static_assert(RL == 4 || RL == 16 || RL == 32, "row width");
-  static_assert(WL == 1 || (WL == 2 && RL == 16), "two words per lane: 16-lane rows");
-  using Word = std::conditional_t<WL == 2, uint64_t, uint32_t>;
+  static_assert(WL == 1 || (WL == 2 && RL == 16) || (WL == 4 && RL == 4),
+                "two words per lane: 16-lane rows; four words per lane: 4-lane rows");
+  using Word = std::conditional_t<WL == 4, u32x4, std::conditional_t<WL == 2, uint64_t, uint32_t>>;
+  // word h of a step's load
+  auto wsel = [](const Word& x, int h) -> uint32_t {
+    if constexpr (WL == 4) return x[h];
+    else return (uint32_t)((uint64_t)x >> (32 * h));
+  };
+
   // Rows of 32 virtual lanes read whole 128-byte lines: the window runs
   // between line boundaries (the range descriptor is line-aligned, cx.adj),
   // the loads are non-temporal, t = 4a + b window bytes follow the frame end
@@ -535,6 +581,9 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   // rows: window end = frame end rounded up to 4 bytes, t = 0..3 on the last
   // lane.
   constexpr bool kLine = VL == 32;
+  // the row width of the LDS image the workgroup loaded (four-word 4-lane
+  // rows: 16 virtual lanes, the RL = 16 image)
+  constexpr int kImg = kLine ? 32 : (WL == 4 ? 16 : RL);
   constexpr uint32_t kEndAlign = kLine ? 128u : 4u;
   static_assert(S >= 1 && NR <= (uint32_t)CH && CH <= 64 && S * NR <= 64, "chunk and bounds window shape");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
@@ -547,6 +596,11 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   const uint32_t lane = L.lane, p = L.p, row = L.row, bu0 = L.bu0, bu1 = L.bu1, bf = L.bf, bt = L.bt;
   const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
   const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
+  // four-word 4-lane rows: a T column of the RL = 16 image whose nibble pair is
+  // (p, p + 4), spread over the banks by row
+  const uint32_t bt4 = kTBase | ((p + ((row & 1u) << 3) + (((row >> 1) & 1u) << 4)) << 2);
+  Lanes Lz = L;  // the lane constants zero_advance uses (append mode)
+  if constexpr (WL == 4) Lz.bt = bt4;
 
   // ---- chunks (uniform): one ds_add_rtn on the workgroup's LDS counter
   auto claim = [&]() -> uint32_t {
@@ -691,9 +745,19 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     rj += ns;
     if constexpr (VAR == 2) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) w[s][k] = (Word)(voff * 0x9E3779B1u + k) * 0x100000001ull;
+      for (int k = 0; k < KS; ++k) {
+        if constexpr (WL == 4) {
+          const uint32_t z = voff * 0x9E3779B1u + k;
+          w[s][k] = u32x4{z, z ^ 1u, z ^ 2u, z ^ 3u};
+        } else {
+          w[s][k] = (Word)(voff * 0x9E3779B1u + k) * 0x100000001ull;
+        }
+      }
     } else {
-      if constexpr (kLine && WL == 1 && EDGE && KS >= 4) {
+      if constexpr (WL == 4) {
+        // four-word 4-lane rows: runs of NSR steps the item has (64-byte row steps)
+        ld_item4_ns<0, KS, (int)SB, NSR>(w[s], voff, ns, data_rsrc);
+      } else if constexpr (kLine && WL == 1 && EDGE && KS >= 4) {
         // whole-line rows: an item's first step (a frame's first line) and
         // its last two (where a frame's last line lies when its items end on
         // a full one, e.g. 9000 B) at the default cache policy, so the line two
@@ -782,7 +846,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     const bool full = !wave_any(!all_full);
     const bool near = !full && !wave_any(!all_near);
     auto word = [&](int k, int h) -> uint32_t {
-      uint32_t x = (uint32_t)(w[s][k] >> (32 * h));
+      uint32_t x = wsel(w[s][k], h);
       if (k == 0) x = (x & keep[h]) ^ initm[h];
       if (k == 1 && h == 0) x ^= m1;
       return x;
@@ -874,6 +938,23 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         // the pair's halves: row 2m gets fA.h0 ^ fA.h1, row 2m+1 fB.h0 ^ fB.h1
         const auto sw = __builtin_amdgcn_permlane16_swap(fA, fB, false, false);
         R = t_fix<16>(lds, sw[0] ^ sw[1], t & 3u, p, bt);
+      } else if constexpr (WL == 4) {
+        // virtual lane v = 4p + h sits 4v bytes past the window end: F_v is
+        // column v (+16) of the RL = 16 image.  Pass j applies F to register
+        // (j + row) & 3, so the 8 rows of a half-wave use 16 functions twice,
+        // on the two copies (row bit 2): 32 distinct banks.  Junk bytes sit in
+        // virtual lane 15 (lane 3, register 3).
+        uint32_t r[4] = {fin.reg[0], fin.reg[1], fin.reg[2], fin.reg[3]};
+        if (wave_any(fin.junk != 0)) r[3] ^= u_step(lds, fin.junk, bu0, bu1);
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t h = (j + row) & 3u;
+          const uint32_t x = h == 0 ? r[0] : h == 1 ? r[1] : h == 2 ? r[2] : r[3];
+          const uint32_t c = 4u * p + h + (((row >> 2) & 1u) << 4);
+          acc ^= f_step(lds, x, kFBase | (c << 2));
+        }
+        R = t_fix<4>(lds, row_xor<4>(acc), t & 3u, p, bt4);
       } else {
         uint32_t r = fin.reg[0];
         if (wave_any(fin.junk != 0)) r ^= u_step(lds, fin.junk, bu0, bu1);
@@ -888,10 +969,10 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       if constexpr (MODE == CrcMode::kAppend) {
         const bool lv = fin.last && fin.f != kNoFrame;
         if constexpr (kHold)
-          R = append_pad<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.ap.data_base + fin.e, kpad);
+          R = append_pad<RL, kImg>(lds, Lz, lv, n, R, cx.ap.data_base + fin.e, kpad);
         else  // VAR 4: the FCS, length and status stored at once (A/B)
-          append_tail<RL, kLine ? 32 : RL>(lds, L, lv, n, R, cx.ap.data_base + fin.e, cx.ap.cap, cx.ap.lenw + fin.f,
-                                           cx.ap.stat + fin.f);
+          append_tail<RL, kImg>(lds, Lz, lv, n, R, cx.ap.data_base + fin.e, cx.ap.cap, cx.ap.lenw + fin.f,
+                                cx.ap.stat + fin.f);
       }
       crc = ~R;
     }
@@ -944,6 +1025,9 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     }(std::make_integer_sequence<int, S>{});
   }
 #undef LNX_FENCE
+  // the slots that held no work at the end still issued their (out-of-range)
+  // loads: retire them before the flush reuses registers (audit_ring.py)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (kHold && wave_any(pc != 0)) flush();
   // drain: no asm load may still be writing registers when the wave ends
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1369,7 +1453,7 @@ constexpr uint64_t kLineMean = 4096;
 constexpr uint64_t kLeanMean = 1600;
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4>
+          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4, int NW4 = 1>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1410,8 +1494,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // the F/T tail is copied verbatim; it is zero at kCtrBase, which starts
     // the chunk counter at 0
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
+    // (4-lane rows of four words per lane fold 16 virtual lanes: the RL = 16 image)
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          image_index(line ? 32 : rl) * kCompactDwords;
+                          image_index(line ? 32 : (narrow && NW4 == 4) ? 16 : rl) * kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
     const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
@@ -1491,10 +1576,10 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // gigabyte frames: static per-wave ranges on the unpipelined path
     const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
-    if (narrow) {
+    if (narrow && NW4 != 4) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_generic<MODE, 4>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out, cap);
-    } else if (!line) {
+    } else if (!line) {  // (also the narrow rows of four words: the RL = 16 image)
       L.p = lane & 15u, L.row = lane >> 4;
       rows_generic<MODE, 16>(lds, L, bytes, off, SEG ? seg_len : nullptr, fw0, fw1, out, cap);
     } else {  // the RL = 32 image: 32-lane rows
@@ -1507,7 +1592,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
-      rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG, 1, true, NSR4>(lds, L, cx);
+      rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG, NW4, true, NSR4>(lds, L, cx);
     } else if (rl == 16 && lean) {
       // lean rows: 16 lanes x two words (LWL = 2) or 32 lanes x one word (LWL = 1)
       L.p = lane & (32u / LWL - 1u), L.row = lane / (32u / LWL);
@@ -1625,6 +1710,17 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 120: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 2); break;
       case 124: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 1); break;
       case 126: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 6); break;
+      // four-word 4-lane rows (dwordx4: 64 contiguous bytes per row instruction) under the product
+      // dispatch: KS4 steps of 64 B, S4 slots, CH4-frame chunks, NSR4-step load runs
+#define LNX_W4(V, KS_, S_, CH_, NSR_) \
+  LNX_LAUNCH(CrcMode::kCrc, V, 0, 24, 1, KS_, S_, 4, CH_, false, 4, 24, 1, 4, 13, 2, true, 1, true, NSR_, 4)
+      case 130: LNX_W4(0, 4, 2, 32, 1); break;
+      case 135: LNX_W4(1, 4, 2, 32, 1); break;  // loads + bookkeeping only
+      case 136: LNX_W4(2, 4, 2, 32, 1); break;  // math + bookkeeping only
+      case 138: LNX_W4(0, 4, 2, 16, 1); break;
+      case 139: LNX_W4(0, 3, 2, 32, 1); break;
+      case 140: LNX_W4(0, 5, 2, 32, 1); break;
+#undef LNX_W4
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
