@@ -441,6 +441,36 @@ def main():
             tr = json.load(fh)
         out["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
         out["roofline"]["traffic_source"] = os.path.relpath(traffic_file, ROOT)
+    # Compute ceilings of the issue pipes (MI355X_MICROARCH.md: a wave issues a
+    # VALU instruction over 2 cycles, so 0.5 wave-instructions per cycle per
+    # SIMD; a ds_read_b32 wave-instruction takes 2 LDS-array cycles, so 0.5 per
+    # cycle per CU; 256 CUs at 2.4 GHz), against the instruction counts per
+    # launch of the committed PMC pass (profiles/counters_<tag>.json) over this
+    # run's kernel time.  For kernels bound by dependent LDS / VALU chains
+    # (CRC32Search) these, not HBM, say how far the kernel is from its ceiling.
+    counters_file = os.path.join(ROOT, "profiles", f"counters_{tag}.json")
+    if os.path.exists(counters_file):
+        with open(counters_file) as fh:
+            cn = json.load(fh)
+        clk, cus = 2.4e9, 256
+        peaks = {"valu": cus * 4 * 0.5 * clk, "lds": cus * 0.5 * clk}
+        counts = {"valu": cn["SQ_INSTS_VALU"], "lds": cn["SQ_INSTS_LDS"]}
+        comp = {}
+        for k in ("valu", "lds"):
+            ach = counts[k] / (kern_ms * 1e-3)
+            comp[k] = {"achieved": round(ach / 1e9, 2), "peak": round(peaks[k] / 1e9, 2), "unit": "G wave-instr/s",
+                       "frac": round(ach / peaks[k], 4), "per_launch": counts[k]}
+        if "SQ_LDS_IDX_ACTIVE" in cn:  # LDS-array busy cycles (bank conflicts included) over the CU-cycles
+            comp["lds"]["array_busy_frac"] = round(cn["SQ_LDS_IDX_ACTIVE"] / (kern_ms * 1e-3 * clk * cus), 4)
+        comp["source"] = os.path.relpath(counters_file, ROOT)
+        out["roofline_compute"] = comp
+        top = max(("valu", "lds"), key=lambda k: comp[k]["frac"])
+        if comp[top]["frac"] > out["roofline"]["frac"]:
+            # the issue pipe, not HBM, is the nearer ceiling: it becomes the roofline, HBM moves beside it
+            r = out["roofline"]
+            r["hbm"] = {"achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"]}
+            r.update(bound=top, achieved=comp[top]["achieved"], peak=comp[top]["peak"], unit=comp[top]["unit"],
+                     frac=comp[top]["frac"])
 
     if args.verify:
         from oracle import oracle as O

@@ -584,7 +584,13 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   // the row width of the LDS image the workgroup loaded (four-word 4-lane
   // rows: 16 virtual lanes, the RL = 16 image)
   constexpr int kImg = kLine ? 32 : (WL == 4 ? 16 : RL);
-  constexpr uint32_t kEndAlign = kLine ? 128u : 4u;
+  // Four-word 4-lane rows read 16-byte chunks: the window (and the range
+  // descriptor's base) is 16-byte aligned so that no lane's chunk straddles the
+  // range start (a dwordx4 whose offset wraps below 0 returns all-zero, the
+  // valid dwords included); the t = 4a + b window bytes past the frame end then
+  // follow the line rows' algebra on 16 virtual lanes.
+  constexpr bool kSkip = kLine || WL == 4;  // lanes past the end skip the last step
+  constexpr uint32_t kEndAlign = kLine ? 128u : WL == 4 ? 16u : 4u;
   static_assert(S >= 1 && NR <= (uint32_t)CH && CH <= 64 && S * NR <= 64, "chunk and bounds window shape");
   static_assert(KS >= 2 && (KS - 1) * SB <= 4095, "buffer immediate offset");
   constexpr int kLoads = (VAR == 2 ? 0 : KS) + 3;  // steps, junk, start + end
@@ -740,7 +746,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     const uint32_t voff = alive ? rea - ((rJ - rj) << kSbLog) + p * 4u * WL : kOOB;
     const bool ends = alive && rj + ns == rJ && rJ != 0;
     // the (virtual) lane whose word holds the frame end, when junk bytes follow it in that word
-    const uint32_t jl = kLine ? 31u - (rt >> 2) : VL - 1u;
+    const uint32_t jl = kSkip ? VL - 1u - (rt >> 2) : VL - 1u;
     const uint32_t jv = ends && p == jl / WL && (rt & 3u) != 0 ? rea - SB + (jl << 2) : kOOB;
     rj += ns;
     if constexpr (VAR == 2) {
@@ -839,7 +845,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
     constexpr int kTail = kLine && KS > 2 ? 2 : KS;
 #pragma unroll
     for (int h = 0; h < WL; ++h) {
-      nsl[h] = kLine && last && ns != 0 && p * WL + h >= 32u - (t >> 2) ? ns - 1u : ns;
+      nsl[h] = kSkip && last && ns != 0 && p * WL + h >= VL - (t >> 2) ? ns - 1u : ns;
       all_full = all_full && alive && nsl[h] == (uint32_t)KS;
       all_near = all_near && alive && nsl[h] + (uint32_t)kTail >= (uint32_t)KS;
     }
@@ -939,19 +945,26 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         const auto sw = __builtin_amdgcn_permlane16_swap(fA, fB, false, false);
         R = t_fix<16>(lds, sw[0] ^ sw[1], t & 3u, p, bt);
       } else if constexpr (WL == 4) {
-        // virtual lane v = 4p + h sits 4v bytes past the window end: F_v is
-        // column v (+16) of the RL = 16 image.  Pass j applies F to register
-        // (j + row) & 3, so the 8 rows of a half-wave use 16 functions twice,
-        // on the two copies (row bit 2): 32 distinct banks.  Junk bytes sit in
-        // virtual lane 15 (lane 3, register 3).
+        // t = 4a + b window bytes follow the frame end; virtual lane v = 4p + h
+        // ends 4((v + a) mod 16) + b bytes past it (lanes v >= 16 - a skipped
+        // the last step), so it takes F from column (v + a) mod 16 (+16) of the
+        // RL = 16 image, then Z_{-b}.  Pass j applies F to the register h with
+        // v + a = j + row (mod 4): the 8 rows of a half-wave use each residue
+        // twice, on the two copies (row bit 2), and p spreads the quotient: 32
+        // distinct banks.  The b junk bytes sit in virtual lane 15 - a.
+        const uint32_t a = t >> 2;
         uint32_t r[4] = {fin.reg[0], fin.reg[1], fin.reg[2], fin.reg[3]};
-        if (wave_any(fin.junk != 0)) r[3] ^= u_step(lds, fin.junk, bu0, bu1);
+        if (wave_any(fin.junk != 0)) {
+          const uint32_t u = u_step(lds, fin.junk, bu0, bu1);  // zero off the junk lane
+          const uint32_t hj = (15u - a) & 3u;
+          r[0] ^= hj == 0 ? u : 0u, r[1] ^= hj == 1 ? u : 0u, r[2] ^= hj == 2 ? u : 0u, r[3] ^= hj == 3 ? u : 0u;
+        }
         uint32_t acc = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
-          const uint32_t h = (j + row) & 3u;
+          const uint32_t h = (j + row - a) & 3u;
           const uint32_t x = h == 0 ? r[0] : h == 1 ? r[1] : h == 2 ? r[2] : r[3];
-          const uint32_t c = 4u * p + h + (((row >> 2) & 1u) << 4);
+          const uint32_t c = ((4u * p + h + a) & 15u) + (((row >> 2) & 1u) << 4);
           acc ^= f_step(lds, x, kFBase | (c << 2));
         }
         R = t_fix<4>(lds, row_xor<4>(acc), t & 3u, p, bt4);
@@ -1534,7 +1547,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   // A range (a workgroup's slice of frames) is addressed through one buffer
   // descriptor whose base is 4-byte aligned (128-byte aligned for 32-lane
   // rows, whose windows run between lines): rel(x) = x - off[fb0] + adj.
-  const uint32_t amask = line ? 127u : 3u;
+  const uint32_t amask = line ? 127u : (narrow && NW4 == 4) ? 15u : 3u;
   struct Range {
     uint64_t f0, f1, o0, o1;
     bool fits;  // byte range within 31-bit buffer offsets

@@ -51,7 +51,10 @@ for STEP in "$@"; do
       run 300 $O/bench_${A}_${B}.jsonl python -u bench.py --workload $A --op $B $EXTRA
       tail -1 $O/bench_${A}_${B}.jsonl ;;
     prof) run 900 $O/prof_${A}_${B:-crc32}.log bash tools/prof/profile.sh $TAG $A ${B:-crc32} ;;
-    py) run 600 $O/py_$(basename $A .py).log python -u $A ${B//,/ }; tail -30 $O/py_$(basename $A .py).log ;;
+    py)  # a python script, or an executable (a microbenchmark binary built in-tree)
+      if [[ $A == *.py ]]; then run 600 $O/py_$(basename $A .py).log python -u $A ${B//,/ };
+      else run 600 $O/py_$(basename $A).log ./$A ${B//,/ }; fi
+      tail -30 $O/py_$(basename $A .py).log ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done
