@@ -453,15 +453,17 @@ def main():
         with open(counters_file) as fh:
             cn = json.load(fh)
         clk, cus = 2.4e9, 256
-        peaks = {"valu": cus * 4 * 0.5 * clk, "lds": cus * 0.5 * clk}
-        counts = {"valu": cn["SQ_INSTS_VALU"], "lds": cn["SQ_INSTS_LDS"]}
-        comp = {}
-        for k in ("valu", "lds"):
-            ach = counts[k] / (kern_ms * 1e-3)
-            comp[k] = {"achieved": round(ach / 1e9, 2), "peak": round(peaks[k] / 1e9, 2), "unit": "G wave-instr/s",
-                       "frac": round(ach / peaks[k], 4), "per_launch": counts[k]}
-        if "SQ_LDS_IDX_ACTIVE" in cn:  # LDS-array busy cycles (bank conflicts included) over the CU-cycles
-            comp["lds"]["array_busy_frac"] = round(cn["SQ_LDS_IDX_ACTIVE"] / (kern_ms * 1e-3 * clk * cus), 4)
+        sec = kern_ms * 1e-3
+        valu = cn["SQ_INSTS_VALU"] / sec
+        comp = {"valu": {"achieved": round(valu / 1e9, 2), "peak": round(cus * 4 * 0.5 * clk / 1e9, 2),
+                         "unit": "G wave-instr/s", "frac": round(valu / (cus * 4 * 0.5 * clk), 4),
+                         "per_launch": cn["SQ_INSTS_VALU"]}}
+        # LDS: the array's busy cycles (SQ_LDS_IDX_ACTIVE, bank-conflict cycles included) against one
+        # array cycle per clock per CU; the instruction count beside it
+        busy = cn["SQ_LDS_IDX_ACTIVE"] / sec
+        comp["lds"] = {"achieved": round(busy / 1e9, 2), "peak": round(cus * clk / 1e9, 2), "unit": "G LDS-array cycles/s",
+                       "frac": round(busy / (cus * clk), 4), "instr_per_launch": cn["SQ_INSTS_LDS"],
+                       "bank_conflict_cycles_per_launch": cn.get("SQ_LDS_BANK_CONFLICT")}
         comp["source"] = os.path.relpath(counters_file, ROOT)
         out["roofline_compute"] = comp
         top = max(("valu", "lds"), key=lambda k: comp[k]["frac"])

@@ -61,6 +61,12 @@ def main():
                        "method": "rocprofv3 --pmc FETCH_SIZE, own pass; x factor measured on tools/prof/calib "
                                  "(dword-per-lane reads of 2 GiB) in the same profiling run"}, fh, indent=1)
     c = summary["counters"]
+    keys = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT")
+    if all(k in c for k in keys):  # read by bench.py (roofline_compute)
+        with open(os.path.join(dst, f"counters_{wl}.json"), "w") as fh:
+            json.dump({**{k: c[k] for k in keys}, "source": f"{tag}_{wl}_summary.json",
+                       "method": "rocprofv3 --pmc, one counter group per pass (tools/prof/profile.sh), per-launch "
+                                 "averages over the traced dispatches; SQ_* summed over all CUs"}, fh, indent=1)
     if "GRBM_GUI_ACTIVE" in c and summary["avg_ns"]:
         summary["clock_ghz_est"] = c["GRBM_GUI_ACTIVE"] / 8 / summary["avg_ns"]
     with open(os.path.join(dst, f"{tag}_{wl}_summary.json"), "w") as fh:
