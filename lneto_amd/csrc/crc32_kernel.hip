@@ -451,7 +451,11 @@ __device__ __forceinline__ void store_held(const WaveCtxAppend& a, bool st, uint
                                            uint32_t hpl) {
   if (st && hpl) {
     uint8_t* q = a.data_base + he;
-    q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
+    if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0) {  // one dword store (LE: the FCS byte order)
+      *reinterpret_cast<uint32_t*>(q) = hv;
+    } else {
+      q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
+    }
     a.lenw[hf] = hpl;
   }
   if (st) a.stat[hf] = hpl ? (uint8_t)0 : kErrShortBuffer;

@@ -430,12 +430,20 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       g_val[1] = ing_sum16(hX);
       const uint32_t tc = ing_sum16(tX + lseed);
       g_val[2] = g_nz && tc == 0 ? 0xFFFFu : tc;
-      // lane p stores byte p & 1 (big-endian) of field p >> 1
-      const uint32_t k = p >> 1;
+      // lane k < 4 stores field k (big-endian): one 16-bit store when the
+      // field's address is even, else its two bytes
+      const uint32_t k = p;
       const uint32_t fo = k == 0 ? g_off[0] : k == 1 ? g_off[1] : k == 2 ? g_off[2] : g_off[3];
       const uint32_t fv = k == 0 ? g_val[0] : k == 1 ? g_val[1] : k == 2 ? g_val[2] : g_val[3];
-      if (live && v == 0 && k < 4 && fo != 0)
-        const_cast<uint8_t*>(fr)[fo + (p & 1u)] = (uint8_t)((p & 1u) ? fv : fv >> 8);
+      if (live && v == 0 && k < 4 && fo != 0) {
+        uint8_t* q = const_cast<uint8_t*>(fr) + fo;
+        if ((reinterpret_cast<uintptr_t>(q) & 1u) == 0) {
+          *reinterpret_cast<uint16_t*>(q) = (uint16_t)(((fv & 0xFFu) << 8) | ((fv >> 8) & 0xFFu));
+        } else {
+          q[0] = (uint8_t)(fv >> 8);
+          q[1] = (uint8_t)fv;
+        }
+      }
     } else {
       if (v == 0 && hdr_sum && ing_sum16(hX) != 0) v = kErrBadCRC;
       if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
