@@ -163,11 +163,15 @@ int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const 
  * IPv4 header sum over the first 20 bytes, TCP / UDP sums with pseudo-header)
  * or demux6 (internet/stack-ip6.go:86-138).  0 = all checks passed or none
  * applies (other EtherTypes); otherwise the lneto errGeneric value
- * (errors.go:6-28): 2 ErrPacketDrop (evil bit, only with LNX_VERIFY_EVIL_BIT),
+ * (errors.go:6-28): 2 ErrPacketDrop (evil bit, only with LNX_VERIFY_EVIL_BIT;
+ * an ICMPv4 type other than echo / echo reply, only with LNX_VERIFY_ICMP),
  * 3 ErrBadCRC, 14 ErrInvalidField, 15 ErrInvalidLengthField,
  * 18 ErrTruncatedFrame.  Destination filtering and handler lookup are stack
- * configuration and are taken as accept-all. */
+ * configuration and are taken as accept-all.  With LNX_VERIFY_ICMP, ICMP
+ * messages also take their client's Demux checks up to the checksum
+ * (ipv4/icmpv4/client.go:89-102, ipv6/icmpv6/client.go:100-115). */
 #define LNX_VERIFY_EVIL_BIT 1u /* lneto.ValidateEvilBit on the stack's Validator */
+#define LNX_VERIFY_ICMP 2u     /* the ICMPv4 / ICMPv6 clients are attached (StackAsync.EnableICMP) */
 int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                              uint8_t* d_verdict, void* stream);
 

@@ -191,9 +191,12 @@ inline int GenerateChecksumsBatch(uint8_t* d_bytes, const uint64_t* d_start, con
 
 // Receive-path checksum verdicts of every Ethernet frame (0 or the lneto
 // errGeneric code), StackEthernet.Demux -> demux4 / demux6.
+// icmp: the ICMP clients' checks too (LNX_VERIFY_ICMP).
 inline int VerifyIngressBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_verdict,
-                              bool evilBit = false, void* stream = nullptr) {
-  return lnx_ingress_verify_batch(d_frames, d_off, n, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, d_verdict, stream);
+                              bool evilBit = false, void* stream = nullptr, bool icmp = false) {
+  return lnx_ingress_verify_batch(d_frames, d_off, n,
+                                  (evilBit ? LNX_VERIFY_EVIL_BIT : 0u) | (icmp ? LNX_VERIFY_ICMP : 0u), d_verdict,
+                                  stream);
 }
 }  // namespace internet
 

@@ -352,6 +352,7 @@ def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
 
 
 VERIFY_EVIL_BIT = 1  # LNX_VERIFY_EVIL_BIT
+VERIFY_ICMP = 2      # LNX_VERIFY_ICMP
 TX_CHECKSUM, TX_FCS = 1, 2  # LNX_TX_CHECKSUM, LNX_TX_FCS
 
 

@@ -447,18 +447,29 @@ __device__ __forceinline__ uint32_t append_pad(const char* lds, const Lanes& L, 
 }
 // Held append results of a lane: frame hf (relative), FCS hv at rel position
 // he, new length hpl (0: the frame did not fit, status ErrShortBuffer).
+// NT (A/B variant 6): non-temporal stores.
+template <bool NT = false>
 __device__ __forceinline__ void store_held(const WaveCtxAppend& a, bool st, uint32_t hf, uint32_t hv, uint32_t he,
                                            uint32_t hpl) {
   if (st && hpl) {
     uint8_t* q = a.data_base + he;
     if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0) {  // one dword store (LE: the FCS byte order)
-      *reinterpret_cast<uint32_t*>(q) = hv;
+      if constexpr (NT) __builtin_nontemporal_store(hv, reinterpret_cast<uint32_t*>(q));
+      else *reinterpret_cast<uint32_t*>(q) = hv;
+    } else if constexpr (NT) {
+      __builtin_nontemporal_store((uint8_t)hv, q), __builtin_nontemporal_store((uint8_t)(hv >> 8), q + 1);
+      __builtin_nontemporal_store((uint8_t)(hv >> 16), q + 2), __builtin_nontemporal_store((uint8_t)(hv >> 24), q + 3);
     } else {
       q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
     }
-    a.lenw[hf] = hpl;
+    if constexpr (NT) __builtin_nontemporal_store(hpl, a.lenw + hf);
+    else a.lenw[hf] = hpl;
   }
-  if (st) a.stat[hf] = hpl ? (uint8_t)0 : kErrShortBuffer;
+  const uint8_t sv = hpl ? (uint8_t)0 : kErrShortBuffer;
+  if (st) {
+    if constexpr (NT) __builtin_nontemporal_store(sv, a.stat + hf);
+    else a.stat[hf] = sv;
+  }
 }
 
 template <int RL, int IMGRL>
@@ -698,7 +709,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   uint32_t win = kWinFlush ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog) : 0u;
   auto flush = [&]() {
     if constexpr (MODE == CrcMode::kAppend)
-      store_held(cx.ap, p < pc, hf, hv, he, hpl);
+      store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
     else
       store_result<MODE>(out_rsrc, p < pc, hf, hv);
     pc = 0;
@@ -1399,7 +1410,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     win = now;
     if (fl) {
       if constexpr (MODE == CrcMode::kAppend)
-        store_held(cx.ap, p < pc, hf, hv, he, hpl);
+        store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
       else
         store_result<MODE>(out_rsrc, p < pc, hf, hv);
       pc = 0;
@@ -1442,7 +1453,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wave_any(pc != 0)) {
     if constexpr (MODE == CrcMode::kAppend)
-      store_held(cx.ap, p < pc, hf, hv, he, hpl);
+      store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
     else
       store_result<MODE>(out_rsrc, p < pc, hf, hv);
   }
@@ -1647,6 +1658,8 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend && var == 4)  // profiling: FCS stored at once, no hold
       LNX_LAUNCH(CrcMode::kAppend, 4, 0, 24, 1, 12, 2, 4, 16, true);
+    else if (mode == CrcMode::kAppend && var == 6)  // profiling: non-temporal result stores
+      LNX_LAUNCH(CrcMode::kAppend, 6, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend)
       LNX_LAUNCH(CrcMode::kAppend, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else

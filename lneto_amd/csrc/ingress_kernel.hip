@@ -12,7 +12,11 @@
 //          the UDP size checks (udp/frame.go:15-20,96-104);
 //   0x86DD demux6 (internet/stack-ip6.go:86-138): ipv6.NewFrame, ValidateSize
 //          (ipv6/frame.go:123-128), TCP / UDP sums with CRCWritePseudo
-//          (ipv6/frame.go:104-108); the UDP sum covers the whole IPv6 payload.
+//          (ipv6/frame.go:104-108); the UDP sum covers the whole IPv6 payload;
+//   with kVerifyIcmp, ICMP messages also take their client's Demux checks up to
+//          the checksum (ipv4/icmpv4/client.go:89-102: size, echo types,
+//          sum with no pseudo-header; ipv6/icmpv6/client.go:100-115: size,
+//          sum with the pseudo-header, as CRCWritePseudo with proto 58).
 // The verdict is 0 (every check passed, or none applies) or the errGeneric
 // code the reference returns (errors.go:6-28).  Destination filtering and
 // handler lookup depend on stack configuration: taken as accept-all.
@@ -42,7 +46,7 @@ constexpr int kIngUnroll = 24;
 constexpr int kIngUnrollQ = 12;
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
-constexpr uint32_t kVerifyEvilBit = 1;
+constexpr uint32_t kVerifyEvilBit = 1, kVerifyIcmp = 2;
 
 __device__ __forceinline__ uint32_t ing_keep_from(int32_t lo) {
   lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
@@ -154,7 +158,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
 
     // ---- header parse: row-uniform; v = verdict so far, sums requested below
     uint32_t v = 0;
-    uint32_t v_udp4 = 0;  // IPv4 UDP size verdict: demux4 reports it only after the header sum passed
+    uint32_t v_udp4 = 0;  // IPv4 UDP / ICMP size verdict: demux4 reports it only after the header sum passed
     bool hdr_sum = false, l4_sum = false;
     int32_t pa = 0, pb = 0, la = 0, lb = 0;  // pseudo-address bytes [pa, pb), transport [la, lb)
     uint32_t lseed = 0;                       // length + protocol words of the pseudo-header
@@ -265,6 +269,18 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
                     lseed = ul + 17u;
                   }
                 }
+              } else if (proto == 1 && (flags & kVerifyIcmp)) {
+                if (P < 8) {
+                  v_udp4 = kErrTruncatedFrame;
+                } else {
+                  const uint32_t type = field16(14 + hl) >> 8;
+                  if (type != 0 && type != 8) {
+                    v_udp4 = kErrPacketDrop;
+                  } else {
+                    l4_sum = true;  // no pseudo-header: [pa, pb) empty, lseed 0
+                    la = 14 + hl, lb = 14 + tl;
+                  }
+                }
               }
             }
           }
@@ -276,9 +292,11 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
             const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
             if (pl + 40 > M) {
               v = kErrInvalidLengthField;
-            } else if (proto == 6 || proto == 17) {
+            } else if (proto == 6 || proto == 17 || (proto == 58 && (flags & kVerifyIcmp))) {
               // demux6 size-checks the UDP header only; TCP goes straight to the
-              // sum (internet/stack-ip6.go:116-137), whatever pl is.
+              // sum (internet/stack-ip6.go:116-137), whatever pl is.  ICMPv6:
+              // icmpv6.NewFrame's size check, then the same pseudo-header sum.
+              if (proto == 58 && pl < 8) v = kErrTruncatedFrame;
               if (proto == 17) {
                 if (pl < 8) v = kErrTruncatedFrame;
                 else if (field16(58) < 8) v = kErrInvalidLengthField;

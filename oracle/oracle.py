@@ -175,12 +175,18 @@ ERR_INVALID_FIELD = 14
 ERR_INVALID_LENGTH_FIELD = 15
 ERR_TRUNCATED_FRAME = 18
 VERIFY_EVIL_BIT = 1  # mirrors lneto.ValidateEvilBit on the stack's Validator
+# ICMP clients attached: their Demux checks up to and including the checksum
+# (ipv4/icmpv4/client.go:89-102, ipv6/icmpv6/client.go:100-115)
+VERIFY_ICMP = 2
+ICMPV4_ECHO_REPLY, ICMPV4_ECHO = 0, 8  # ipv4/icmpv4/icmpv4.go:18-19
 
 ETHERTYPE_IPV4 = 0x0800
 ETHERTYPE_IPV6 = 0x86DD
 ETHERTYPE_VLAN = 0x8100
 IPPROTO_TCP = 6
 IPPROTO_UDP = 17
+IPPROTO_ICMP = 1     # definitions.go:48
+IPPROTO_ICMPV6 = 58  # definitions.go:105
 
 
 def _be16(b: bytes, i: int) -> int:
@@ -225,10 +231,19 @@ def _ipv4_verdict(ip: bytes, flags: int) -> int:
             return ERR_TRUNCATED_FRAME
         if ipv4_udp_pseudo(ip, ul).payload_sum16(payload[:ul]) != 0:
             return ERR_BAD_CRC
+    elif proto == IPPROTO_ICMP and flags & VERIFY_ICMP:
+        # demux4 hands frame[:tl] at offset hl to the ICMP client
+        # (stack-ip4.go:168-170); its Demux (ipv4/icmpv4/client.go:89-102):
+        if len(payload) < 8:                           # icmpv4.NewFrame (icmpv4.go:62-67)
+            return ERR_TRUNCATED_FRAME
+        if payload[0] not in (ICMPV4_ECHO, ICMPV4_ECHO_REPLY):
+            return ERR_PACKET_DROP
+        if CRC791().payload_sum16(payload) != 0:       # no pseudo-header
+            return ERR_BAD_CRC
     return 0
 
 
-def _ipv6_verdict(ip6: bytes) -> int:
+def _ipv6_verdict(ip6: bytes, flags: int = 0) -> int:
     """demux6 up to its checksum checks (internet/stack-ip6.go:86-138)."""
     if len(ip6) < 40:                                  # ipv6.NewFrame (ipv6/frame.go:13-18)
         return ERR_TRUNCATED_FRAME
@@ -251,6 +266,16 @@ def _ipv6_verdict(ip6: bytes) -> int:
         # quirk kept: the IPv6 UDP sum covers the whole IPv6 payload, not the UDP length
         if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
             return ERR_BAD_CRC
+    elif proto == IPPROTO_ICMPV6 and flags & VERIFY_ICMP:
+        # the ICMPv6 client gets ip6[:40 + pl] at offset 40 (stack-ip6.go:140-141);
+        # its Demux (ipv6/icmpv6/client.go:100-115) checks the size, then the sum
+        # with the pseudo-header src, dst, AddUint32(len), AddUint32(58) — the
+        # same words as CRCWritePseudo here, pl being the message length.  The
+        # type dispatch (echo / NDP, else ErrPacketDrop) comes after the sum.
+        if len(payload) < 8:                           # icmpv6.NewFrame (icmpv6.go:63-68)
+            return ERR_TRUNCATED_FRAME
+        if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
+            return ERR_BAD_CRC
     return 0
 
 
@@ -260,7 +285,8 @@ def ingress_verdict(frame: bytes, flags: int = 0) -> int:
     size checks, then demux4 / demux6 by EtherType.  0 = every check passed or
     none applies (other EtherTypes); else the errGeneric code returned.
     Destination filtering and handler lookup (ErrPacketDrop) are stack
-    configuration and are taken as accept-all."""
+    configuration and are taken as accept-all.  flags: VERIFY_EVIL_BIT,
+    VERIFY_ICMP (ICMP messages also take the ICMP clients' checks)."""
     if len(frame) < 14:                                # ethernet.NewFrame (ethernet/frame.go:13-18)
         return ERR_TRUNCATED_FRAME
     et = _be16(frame, 12)
@@ -271,13 +297,11 @@ def ingress_verdict(frame: bytes, flags: int = 0) -> int:
     if et == ETHERTYPE_IPV4:
         return _ipv4_verdict(frame[14:], flags)
     if et == ETHERTYPE_IPV6:
-        return _ipv6_verdict(frame[14:])
+        return _ipv6_verdict(frame[14:], flags)
     return 0
 
 
 # ------------------------------------------------- TX checksum generate (a16)
-IPPROTO_ICMP = 1
-IPPROTO_ICMPV6 = 58
 
 
 def _put16(b: bytearray, i: int, v: int) -> None:

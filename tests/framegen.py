@@ -28,6 +28,9 @@ def ipv4(proto: int, l4: bytes, opts: bytes = b"", flags: int = 0x4000, fix_l4: 
     if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
         l4[16:18] = b"\0\0"
         l4[16:18] = struct.pack(">H", O.ipv4_tcp_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
+    if fix_l4 and proto == O.IPPROTO_ICMP and len(l4) >= 8:  # no pseudo-header (ltesto.go:224-227)
+        l4[2:4] = b"\0\0"
+        l4[2:4] = struct.pack(">H", O.CRC791().payload_sum16(bytes(l4)))
     if fix_l4 and proto == O.IPPROTO_UDP and len(l4) >= 8:
         ul = struct.unpack(">H", l4[4:6])[0]
         l4[6:8] = b"\0\0"
@@ -42,6 +45,9 @@ def ipv6(proto: int, l4: bytes, fix_l4: bool = True) -> bytes:
     if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
         l4[16:18] = b"\0\0"
         l4[16:18] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
+    if fix_l4 and proto == O.IPPROTO_ICMPV6 and len(l4) >= 8:  # ipv6/icmpv6/client.go:141-148
+        l4[2:4] = b"\0\0"
+        l4[2:4] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
     if fix_l4 and proto == O.IPPROTO_UDP and len(l4) >= 8:
         l4[6:8] = b"\0\0"  # the stack sums the whole payload (stack-ip6.go:133-134)
         l4[6:8] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4)))
@@ -55,6 +61,71 @@ def tcp(payload: bytes) -> bytes:
 def udp(payload: bytes, length: int | None = None) -> bytes:
     ul = 8 + len(payload) if length is None else length
     return struct.pack(">HHHH", 5353, 53, ul, 0) + payload
+
+
+def icmp(type_: int, payload: bytes, ident: int = 0x1234, seq: int = 1) -> bytes:
+    """An ICMPv4 / ICMPv6 message with an echo-shaped header (type, code 0,
+    checksum, identifier, sequence number); ipv4() / ipv6() fill the checksum."""
+    return struct.pack(">BBHHH", type_, 0, 0, ident, seq) + payload
+
+
+def ltesto_icmp_echo(payload: bytes, ident: int, seq: int) -> bytes:
+    """ltesto.PacketGen.AppendIPv4ICMPEcho (internal/ltesto/ltesto.go:175-231)
+    with the addresses of TestStackAsync_ICMPEchoChecksum
+    (x/xnet/xnet_test.go:1015-1045): IHL 5, ID 0, flags 0, TTL 64, protocol
+    ICMP, header CRC; echo request (type 8, code 0) whose checksum covers the
+    whole ICMP message."""
+    tl = 20 + 8 + len(payload)
+    hdr = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, tl, 0, 0, 64, O.IPPROTO_ICMP, 0,
+                                bytes([192, 168, 1, 1]), bytes([192, 168, 1, 99])))
+    hdr[10:12] = struct.pack(">H", O.ipv4_header_sum16(bytes(hdr)))
+    msg = bytearray(struct.pack(">BBHHH", 8, 0, 0, ident, seq) + payload)
+    msg[2:4] = struct.pack(">H", O.CRC791().payload_sum16(bytes(msg)))
+    return bytes([0xAA, 0xBB, 0xCC, 0xDD, 0xEE, 0xFF, 0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x08, 0x00]) \
+        + bytes(hdr) + bytes(msg)
+
+
+def icmp_frames(seed: int = 3, count: int = 1200) -> list[bytes]:
+    """ICMPv4 / ICMPv6 frames for the ICMP clients' checks (LNX_VERIFY_ICMP):
+    echo and echo reply, other types (ICMPv4 drops them before the sum), one
+    flipped byte, messages under 8 bytes, trailing bytes past tl / pl + 40
+    (ignored), IPv4 options, and a broken IPv4 header in front of a non-echo
+    type (the header sum comes first)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        pay = rng.integers(0, 256, size=int(rng.integers(0, 1400)), dtype=np.uint8).tobytes()
+        kind = i % 12
+        if kind in (0, 1):
+            f = ether(0x0800, ipv4(1, icmp(8 if kind == 0 else 0, pay)))
+        elif kind == 2:
+            f = ether(0x0800, ipv4(1, icmp(int(rng.choice([3, 5, 11, 13, 14, 42, 255])), pay)))
+        elif kind == 3:
+            b = bytearray(ether(0x0800, ipv4(1, icmp(8, pay))))
+            b[int(rng.integers(34, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(b)
+        elif kind == 4:
+            f = ether(0x0800, ipv4(1, rng.integers(0, 256, size=int(rng.integers(0, 8)), dtype=np.uint8).tobytes()))
+        elif kind == 5:
+            f = ether(0x0800, ipv4(1, icmp(0, pay))) + bytes.fromhex("deadbeef")
+        elif kind == 6:
+            f = ether(0x86DD, ipv6(58, icmp(int(rng.choice([1, 128, 129, 135, 136, 200])), pay)))
+        elif kind == 7:
+            b = bytearray(ether(0x86DD, ipv6(58, icmp(128, pay))))
+            b[int(rng.integers(54, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(b)
+        elif kind == 8:
+            f = ether(0x86DD, ipv6(58, rng.integers(0, 256, size=int(rng.integers(0, 8)), dtype=np.uint8).tobytes()))
+        elif kind == 9:
+            f = ether(0x86DD, ipv6(58, icmp(129, pay))) + rng.integers(1, 256, size=20, dtype=np.uint8).tobytes()
+        elif kind == 10:
+            b = bytearray(ether(0x0800, ipv4(1, icmp(3, pay))))
+            b[22] ^= 0x01  # TTL
+            f = bytes(b)
+        else:
+            f = ether(0x0800, ipv4(1, icmp(8, pay), opts=bytes(4 * int(rng.integers(1, 11)))))
+        out.append(f)
+    return out
 
 
 def short_tcp6(rng) -> bytes:

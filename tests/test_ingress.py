@@ -221,3 +221,74 @@ def test_gpu_ingress_jumbo_frames(cuda, base_pad):
     assert (want == 3).sum() > 50 and (want == 0).sum() > 100
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
+
+
+# ---------------------------------------------------------------- ICMP verdicts
+def _icmp_echo_cases():
+    """TestStackAsync_ICMPEchoChecksum (x/xnet/xnet_test.go:1015-1110): a valid
+    echo request, the same with 4 trailing FCS-like bytes (accepted: the client
+    sums Payload(), sliced to tl), and both with the last payload byte flipped
+    (rejected)."""
+    pay = b"abcdefghijklmnopqrstuvwxyz012345"
+    good = G.ltesto_icmp_echo(pay, 0x1234, 1)
+    trailing = G.ltesto_icmp_echo(pay, 0x1234, 2) + bytes.fromhex("deadbeef")
+    bad = bytearray(G.ltesto_icmp_echo(pay, 0x1234, 3)); bad[-1] ^= 0xFF
+    bad_trailing = bytearray(G.ltesto_icmp_echo(pay, 0x1234, 4)); bad_trailing[-1] ^= 0xFF
+    return [good, trailing, bytes(bad), bytes(bad_trailing) + bytes.fromhex("deadbeef")]
+
+
+def test_reference_icmp_echo_checksum_cases():
+    frames = _icmp_echo_cases()
+    assert [O.ingress_verdict(f, O.VERIFY_ICMP) for f in frames] == [0, 0, O.ERR_BAD_CRC, O.ERR_BAD_CRC]
+    # without the ICMP clients the checksum stage has nothing to say about ICMP
+    assert [O.ingress_verdict(f) for f in frames] == [0, 0, 0, 0]
+
+
+def test_icmp_order_and_codes():
+    v4 = G.ether(0x0800, G.ipv4(1, G.icmp(8, b"ping")))
+    assert O.ingress_verdict(v4, O.VERIFY_ICMP) == 0
+    # a non-echo ICMPv4 type is dropped before its sum (ipv4/icmpv4/client.go:95-98)
+    b = bytearray(G.ether(0x0800, G.ipv4(1, G.icmp(11, b"ttl exceeded")))); b[-1] ^= 1
+    assert O.ingress_verdict(bytes(b), O.VERIFY_ICMP) == O.ERR_PACKET_DROP
+    assert O.ingress_verdict(G.ether(0x0800, G.ipv4(1, b"1234567")), O.VERIFY_ICMP) == O.ERR_TRUNCATED_FRAME
+    # the IPv4 header sum comes first
+    b = bytearray(G.ether(0x0800, G.ipv4(1, b"1234567"))); b[22] ^= 1
+    assert O.ingress_verdict(bytes(b), O.VERIFY_ICMP) == O.ERR_BAD_CRC
+    # ICMPv6: size, then the pseudo-header sum; every type passes this stage
+    for t in (1, 128, 129, 135, 136, 200):
+        assert O.ingress_verdict(G.ether(0x86DD, G.ipv6(58, G.icmp(t, b"x" * t))), O.VERIFY_ICMP) == 0
+    assert O.ingress_verdict(G.ether(0x86DD, G.ipv6(58, b"1234567")), O.VERIFY_ICMP) == O.ERR_TRUNCATED_FRAME
+    b = bytearray(G.ether(0x86DD, G.ipv6(58, G.icmp(128, b"abc")))); b[30] ^= 4  # source address
+    assert O.ingress_verdict(bytes(b), O.VERIFY_ICMP) == O.ERR_BAD_CRC
+    assert O.ingress_verdict(bytes(b)) == 0
+
+
+def test_icmp_generator_covers_every_verdict():
+    hist = collections.Counter(O.ingress_verdict(f, O.VERIFY_ICMP) for f in G.icmp_frames(count=1200))
+    for code in (0, O.ERR_PACKET_DROP, O.ERR_BAD_CRC, O.ERR_TRUNCATED_FRAME):
+        assert hist[code] > 50, (code, hist)
+
+
+def test_icmp_generate_then_verify():
+    """The TX generate step (oracle.tx_checksum, the ICMP clients' SetCRC) and
+    the ICMP verdicts agree: a generated echo passes."""
+    for f in G.icmp_frames(seed=5, count=240)[::12]:
+        regen, st = O.tx_checksum(f)
+        if st == 0:
+            assert O.ingress_verdict(regen, O.VERIFY_ICMP) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base_pad", [0, 1, 6])
+@pytest.mark.parametrize("flags", [2, 3])
+def test_gpu_icmp_verdicts_match_oracle(cuda, base_pad, flags):
+    import torch
+    import lneto_amd as L
+    frames = G.icmp_frames(seed=50 + base_pad, count=2400) + _icmp_echo_cases() \
+        + G.frames(seed=60 + base_pad, count=2400)
+    data, off = _pack(frames, base_pad)
+    got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda), torch.from_numpy(off.astype(np.int64)).to(cuda),
+                                 flags=flags).cpu().numpy()
+    want = np.array([O.ingress_verdict(f, flags) for f in frames], dtype=np.uint8)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]

@@ -13,6 +13,7 @@
 #   line:WL:OP[:ARGS] one bench line (ARGS: extra flags, comma-separated)
 #   prof:WL[:OP]      rocprofv3 kernel trace + PMC passes (tools/prof/profile.sh)
 #   py:FILE[:ARGS]    python FILE (a measurement script), ARGS comma-separated
+#   sh:FILE[:ARGS]    bash FILE (a measurement script), ARGS comma-separated
 set -o pipefail
 TAG=$1; shift
 O=gpurun_out/$TAG
@@ -55,6 +56,7 @@ for STEP in "$@"; do
       if [[ $A == *.py ]]; then run 600 $O/py_$(basename $A .py).log python -u $A ${B//,/ };
       else run 600 $O/py_$(basename $A).log ./$A ${B//,/ }; fi
       tail -30 $O/py_$(basename $A .py).log ;;
+    sh) run 600 $O/sh_$(basename $A .sh).log bash $A ${B//,/ }; tail -30 $O/sh_$(basename $A .sh).log ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done

@@ -1,11 +1,12 @@
 # Per-dispatch instruction counters for CRC kernel variants (one PMC pass, no tracing).
-#   tools/prof/pmc_variants.sh TAG WORKLOAD V1,V2,...
+#   tools/prof/pmc_variants.sh TAG WORKLOAD V1+V2+... [C1+C2+... [SUFFIX]]
 set -eu
 TAG=$1; WL=$2; VARS=$3
-OUT=gpurun_out/pmcvar_${TAG}_${WL}
+CTRS=${4:-SQ_INSTS_VALU+SQ_INSTS_SALU+SQ_INSTS_LDS+SQ_INSTS_VMEM_RD}
+OUT=gpurun_out/pmcvar_${TAG}_${WL}${5:+_$5}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD -d $OUT/pmc -o pmc --output-format csv -- python3 tools/prof/variants.py $WL $VARS 1 > $OUT/run.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc ${CTRS//+/ } -d $OUT/pmc -o pmc --output-format csv -- python3 tools/prof/variants.py $WL $VARS 1 > $OUT/run.log 2>&1
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 out = sys.argv[1]
