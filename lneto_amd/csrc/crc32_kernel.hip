@@ -399,7 +399,11 @@ struct WaveCtxAppend {
   uint32_t* lenw;
   uint8_t* stat;
   uint32_t cap;
+  uint32_t rend;  // rel end of the range's bytes (its last frame's end)
 };
+// he value of a held frame whose FCS is already in memory (written with its
+// 64-byte sector, lines_body): the flush writes its length and status only
+constexpr uint32_t kFcsWritten = 0xFFFFFFFFu;
 
 // Z_k(x), k = 1 .. 4 SB (k zero bytes appended to the register x; k = 0:
 // identity), for a row-uniform x and k, with the tables of the image the
@@ -447,29 +451,20 @@ __device__ __forceinline__ uint32_t append_pad(const char* lds, const Lanes& L, 
 }
 // Held append results of a lane: frame hf (relative), FCS hv at rel position
 // he, new length hpl (0: the frame did not fit, status ErrShortBuffer).
-// NT (A/B variant 6): non-temporal stores.
-template <bool NT = false>
 __device__ __forceinline__ void store_held(const WaveCtxAppend& a, bool st, uint32_t hf, uint32_t hv, uint32_t he,
                                            uint32_t hpl) {
   if (st && hpl) {
-    uint8_t* q = a.data_base + he;
-    if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0) {  // one dword store (LE: the FCS byte order)
-      if constexpr (NT) __builtin_nontemporal_store(hv, reinterpret_cast<uint32_t*>(q));
-      else *reinterpret_cast<uint32_t*>(q) = hv;
-    } else if constexpr (NT) {
-      __builtin_nontemporal_store((uint8_t)hv, q), __builtin_nontemporal_store((uint8_t)(hv >> 8), q + 1);
-      __builtin_nontemporal_store((uint8_t)(hv >> 16), q + 2), __builtin_nontemporal_store((uint8_t)(hv >> 24), q + 3);
-    } else {
-      q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
+    if (he != kFcsWritten) {
+      uint8_t* q = a.data_base + he;
+      if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0) {  // one dword store (LE: the FCS byte order)
+        *reinterpret_cast<uint32_t*>(q) = hv;
+      } else {
+        q[0] = (uint8_t)hv, q[1] = (uint8_t)(hv >> 8), q[2] = (uint8_t)(hv >> 16), q[3] = (uint8_t)(hv >> 24);
+      }
     }
-    if constexpr (NT) __builtin_nontemporal_store(hpl, a.lenw + hf);
-    else a.lenw[hf] = hpl;
+    a.lenw[hf] = hpl;
   }
-  const uint8_t sv = hpl ? (uint8_t)0 : kErrShortBuffer;
-  if (st) {
-    if constexpr (NT) __builtin_nontemporal_store(sv, a.stat + hf);
-    else a.stat[hf] = sv;
-  }
+  if (st) a.stat[hf] = hpl ? (uint8_t)0 : kErrShortBuffer;
 }
 
 template <int RL, int IMGRL>
@@ -709,7 +704,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
   uint32_t win = kWinFlush ? (uint32_t)(__builtin_amdgcn_s_memrealtime() >> kWinLog) : 0u;
   auto flush = [&]() {
     if constexpr (MODE == CrcMode::kAppend)
-      store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
+      store_held(cx.ap, p < pc, hf, hv, he, hpl);
     else
       store_result<MODE>(out_rsrc, p < pc, hf, hv);
     pc = 0;
@@ -1226,8 +1221,18 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     }
   };
 
+  // VAR 7 (kAppend, two-word rows; A/B, not the product): the FCS is written
+  // with the whole 64-byte sector that holds it (the frame's last line is in
+  // the lanes' registers: the bytes before the FCS are the frame's, the ones
+  // after it the slot's, rewritten as loaded).  In tools/ubench/scatter_write.hip
+  // whole-sector writes cost a read stream +24 % against +33 % for a dword; in
+  // this kernel they measured 2 % slower than the held dword
+  // (profiles/r3j_fcs_append_sector_ab.txt): every TCC write request became a
+  // 64-byte one, and the time per write stayed.
+  constexpr bool kSector = MODE == CrcMode::kAppend && WL == 2 && VAR == 7;
   struct Fin {
     uint32_t r0, r1, junk, f, n, t, e;
+    uint64_t tl;  // kSector: this lane's 8 bytes of the frame's last line
   };
   auto fold = [&](const Rowp& r) -> Fin {
     const uint32_t n = r.n, t = r.t, J = r.J, a = t >> 2;
@@ -1271,6 +1276,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       return JM ? x & ((uint32_t)k == jlast ? jm[h] : 0xFFFFFFFFu) : x;
     };
     uint32_t reg[WL] = {};
+    uint64_t tl = 0;  // kSector: step J - 1's 8 bytes of this lane
     if constexpr (VAR == 1) {
 #pragma unroll
       for (int k = 0; k < KS; ++k)
@@ -1296,6 +1302,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
             const uint32_t r2 = u_step_xor(lds, reg[h] ^ wordj(k, h), 0u, bu0, bu1);
             reg[h] = (uint32_t)k < nsl[h] ? r2 : reg[h];
           }
+        if constexpr (kSector) tl = (uint64_t)(J == (uint32_t)KS ? w[KS - 1] : w[KS - 2]);
       } else {
         // any J: step k is skipped when no row has k lines, unpredicated while
         // every row with lines has more than k + 1, predicated otherwise
@@ -1305,6 +1312,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
 #pragma unroll
         for (int k = 0; k < KS; ++k) {
           if ((uint32_t)k >= jmax) continue;  // (no break: the loop must stay unrolled)
+          if constexpr (kSector) tl = (uint32_t)k + 1u == J ? (uint64_t)w[k] : tl;
           if ((uint32_t)k + 1u < jmin) {
 #pragma unroll
             for (int h = 0; h < WL; ++h) reg[h] = u_step_xor(lds, reg[h] ^ word(k, h), 0u, bu0, bu1);
@@ -1330,6 +1338,10 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
 #pragma unroll
           for (int k = 0; k < KX; ++k) asm volatile("" : "+v"(wx[k]));
 #pragma unroll
+          for (int k = 0; k < KX; ++k) {
+            if constexpr (kSector) tl = j0 + (uint32_t)k + 1u == J ? (uint64_t)wx[k] : tl;
+          }
+#pragma unroll
           for (int k = 0; k < KX; ++k)
 #pragma unroll
             for (int h = 0; h < WL; ++h) {
@@ -1349,6 +1361,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     fin.n = n;
     fin.t = t;
     fin.e = r.e;
+    fin.tl = tl;
     return fin;
   };
 
@@ -1396,10 +1409,31 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       R = append_pad<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, kpad);
     }
     const uint32_t crc = ~R;
+    bool sec = false;  // kSector: this row's FCS went out with its sector
+    if constexpr (kSector) {
+      // the sector [e & ~63, + 64) (rel and absolute alignment agree: the
+      // range base is line-aligned) when it holds the whole FCS (e mod 64 in
+      // 1..60: then it lies inside the frame's last line, e mod 128 != 0), lies
+      // in the frame's slot ([start, start + cap), start = e - n) and inside the
+      // range's bytes (the range's last frame: bytes past its end read as 0)
+      const uint32_t em = fin.e & 63u;
+      sec = live && kpad == 0 && em - 1u < 60u && (uint64_t)n + 64u - em <= cx.ap.cap &&
+            fin.e - em + 64u <= cx.ap.rend;
+      if (wave_any(sec)) {
+        const uint32_t l0 = fin.e & ~127u, pc0 = l0 + 8u * p;  // this lane's piece of the last line
+        const int32_t d = (int32_t)(fin.e - pc0);               // FCS byte 0 at piece byte d
+        const uint64_t c64 = crc;
+        const uint64_t m = d >= 0 ? (d < 8 ? 0xFFFFFFFFull << (8 * d) : 0ull)
+                                  : (d > -4 ? 0xFFFFFFFFull >> (-8 * d) : 0ull);
+        const uint64_t fv = d >= 0 ? (d < 8 ? c64 << (8 * d) : 0ull) : (d > -4 ? c64 >> (-8 * d) : 0ull);
+        if (sec && pc0 - (fin.e - em) < 64u)
+          *reinterpret_cast<uint64_t*>(cx.ap.data_base + pc0) = (fin.tl & ~m) | (fv & m);
+      }
+    }
     if (live && p == pc) {
       hf = fin.f, hv = result_of<MODE>(n, crc);
       if constexpr (MODE == CrcMode::kAppend) {
-        he = fin.e + kpad;
+        he = sec ? kFcsWritten : fin.e + kpad;
         hpl = (uint64_t)n + kpad + 4u <= cx.ap.cap ? n + kpad + 4u : 0u;
       }
     }
@@ -1410,7 +1444,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
     win = now;
     if (fl) {
       if constexpr (MODE == CrcMode::kAppend)
-        store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
+        store_held(cx.ap, p < pc, hf, hv, he, hpl);
       else
         store_result<MODE>(out_rsrc, p < pc, hf, hv);
       pc = 0;
@@ -1453,7 +1487,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wave_any(pc != 0)) {
     if constexpr (MODE == CrcMode::kAppend)
-      store_held<VAR == 6>(cx.ap, p < pc, hf, hv, he, hpl);
+      store_held(cx.ap, p < pc, hf, hv, he, hpl);
     else
       store_result<MODE>(out_rsrc, p < pc, hf, hv);
   }
@@ -1597,6 +1631,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     cx.ap.lenw = const_cast<uint32_t*>(SEG ? seg_len + r.f0 : seg_len);
     cx.ap.stat = reinterpret_cast<uint8_t*>(out) + r.f0;
     cx.ap.cap = cap;
+    cx.ap.rend = (uint32_t)(bytes_ + cx.adj);
     return cx;
   };
   const Range own = range_of(blockIdx.x, ob0, ob1);
@@ -1658,8 +1693,8 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend && var == 4)  // profiling: FCS stored at once, no hold
       LNX_LAUNCH(CrcMode::kAppend, 4, 0, 24, 1, 12, 2, 4, 16, true);
-    else if (mode == CrcMode::kAppend && var == 6)  // profiling: non-temporal result stores
-      LNX_LAUNCH(CrcMode::kAppend, 6, 0, 24, 1, 12, 2, 4, 16, true);
+    else if (mode == CrcMode::kAppend && var == 7)  // profiling: the FCS written with its 64-byte sector
+      LNX_LAUNCH(CrcMode::kAppend, 7, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend)
       LNX_LAUNCH(CrcMode::kAppend, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else

@@ -112,3 +112,42 @@ def test_gpu_crc32_segments(cuda):
                            torch.from_numpy(lens.astype(np.int32)).to(cuda)).cpu().numpy().view(np.uint32)
     want = [O.crc32(data[s:s + l].tobytes()) for s, l in zip(starts, lens)]
     assert got.tolist() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var", [4, 7])
+@pytest.mark.parametrize("cap,base", [(1536, 0), (1536, 1), (1600, 5)])
+def test_gpu_fcs_append_ab_variants(cuda, var, cap, base):
+    """The append A/B variants (lnx__fcs_append_variant) write what the product
+    writes: 4 = FCS, length and status stored as each frame finishes; 7 = the
+    FCS written with its whole 64-byte sector (bytes after it rewritten as
+    loaded; frames whose FCS straddles a sector, the range's last frame and
+    sectors past the slot take the held path)."""
+    import ctypes
+    import torch
+    import lneto_amd as L
+    fn = L.lib.lnx__fcs_append_variant
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                   ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng([var, cap, base])
+    n = 6000
+    lens = _lens(rng, n, cap, "mtu")
+    lens[7::11] = cap - 4 - rng.integers(0, 64, size=len(lens[7::11]))  # the FCS at every sector position
+    data = rng.integers(0, 256, size=base + n * cap + 8, dtype=np.uint8)
+    starts = base + np.arange(n, dtype=np.int64) * cap
+    d = torch.from_numpy(data.copy()).to(cuda)
+    dl = torch.from_numpy(lens.astype(np.int32)).to(cuda)
+    ds = torch.from_numpy(starts).to(cuda)
+    st = torch.empty(n, dtype=torch.uint8, device=cuda)
+    assert fn(var, d.data_ptr(), ds.data_ptr(), dl.data_ptr(), n, cap, st.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    got, got_len, status = d.cpu().numpy(), dl.cpu().numpy(), st.cpu().numpy()
+    want_img = data.copy()
+    for i in range(n):
+        s = int(starts[i])
+        want, stw = O.fcs_append(data[s:s + int(lens[i])].tobytes(), cap)
+        want_img[s:s + len(want)] = np.frombuffer(want, dtype=np.uint8)
+        assert int(status[i]) == stw and int(got_len[i]) == len(want), i
+    diff = np.nonzero(got != want_img)[0]
+    assert diff.size == 0, [(int(x), int((x - base) // cap)) for x in diff[:10]]

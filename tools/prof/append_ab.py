@@ -1,6 +1,6 @@
 """A/B of the TX FCS append variants (lnx__fcs_append_variant: 0 = product,
 results held and flushed; 4 = FCS / length / status stored as each frame
-finishes; 6 = held, non-temporal stores; -1 = no append: lnx_crc32_segments
+finishes; 7 = the FCS written with its whole 64-byte sector; -1 = no append: lnx_crc32_segments
 over the same frames, the body's cost alone) on bench.py's fcs_append workload: 1 M frames of 1496 B in 1536-B
 slots, lengths reset before every launch.  Round-robin, median of REPS.
 

@@ -6,7 +6,7 @@
 #   tools/prof/gpu_session.sh TAG STEP [STEP ...]
 #
 # Steps:
-#   tests[:EXPR]      pytest -m gpu (optionally -k EXPR)
+#   tests[:EXPR]      pytest -m gpu (optionally -k EXPR; "_or_" stands for " or ")
 #   smoke             __graft_entry__.smoke()
 #   bench             the default bench line (what the driver runs)
 #   lines             a --verify'd bench line per workload / op
@@ -31,7 +31,7 @@ for STEP in "$@"; do
   case $KIND in
     tests)
       if [ -n "$A" ]; then
-        run 900 $O/gpu_tests.log python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -k "$A"
+        run 900 $O/gpu_tests.log python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -k "${A//_or_/ or }"
       else
         run 900 $O/gpu_tests.log python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread
       fi

@@ -8,6 +8,11 @@
 //   3: into a compact array (4 B per slot)
 //   4: in place as four byte stores
 //   5: in place at byte 24 (the IPv4 header checksum of a frame at slot start)
+//   6: in place, the whole 16-byte piece holding byte 1496 rewritten (the
+//      loaded bytes with the result dword replaced)
+//   7: in place, the whole 32-byte sector [1472, 1504) rewritten
+//   8: in place, the whole 64-byte sector [1472, 1536) rewritten
+//   9: in place, the whole 128-byte line [1408, 1536) rewritten
 // Not part of the product.  usage: scatter_write [nslots]
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -45,6 +50,15 @@ __global__ void __launch_bounds__(1024) rd(const u32x4* __restrict__ src, uint8_
         if (k == 1496 / 16) compact[slot] = acc;
       } else if constexpr (MODE == 5) {
         if (k == 1) *reinterpret_cast<uint32_t*>(data + (size_t)slot * kSlot + 24) = acc;
+      } else if constexpr (MODE >= 6) {
+        // pieces k0 .. 95 of the slot are rewritten whole; piece 93 carries the result
+        constexpr uint32_t k0 = MODE == 6 ? 93 : MODE == 7 ? 92 : MODE == 8 ? 92 : 88;
+        constexpr uint32_t k1 = MODE == 6 ? 94 : MODE == 7 ? 94 : 96;
+        if (k >= k0 && k < k1) {
+          u32x4 o = v[u];
+          if (k == 93) o[2] = acc;  // bytes 1496..1499
+          reinterpret_cast<u32x4*>(data)[c] = o;
+        }
       }
     }
   }
@@ -72,13 +86,17 @@ int main(int argc, char** argv) {
       case 3: rd<3><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
       case 4: rd<4><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
       case 5: rd<5><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 6: rd<6><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 7: rd<7><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 8: rd<8><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 9: rd<9><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
     }
   };
   for (int k = 0; k < 200; ++k) launch(0);
   (void)hipDeviceSynchronize();
-  std::vector<std::vector<float>> t(6);
+  std::vector<std::vector<float>> t(10);
   for (int r = 0; r < 9; ++r)
-    for (int m = 0; m < 6; ++m) {
+    for (int m = 0; m < 10; ++m) {
       (void)hipEventRecord(a);
       for (int k = 0; k < 10; ++k) launch(m);
       (void)hipEventRecord(b);
@@ -87,11 +105,13 @@ int main(int argc, char** argv) {
       (void)hipEventElapsedTime(&ms, a, b);
       t[m].push_back(ms / 10);
     }
-  const char* what[6] = {"reads only", "in place, dword at 1496", "in place, non-temporal dword",
-                         "compact array (4 B per slot)", "in place, four byte stores", "in place, dword at 24"};
+  const char* what[10] = {"reads only", "in place, dword at 1496", "in place, non-temporal dword",
+                          "compact array (4 B per slot)", "in place, four byte stores", "in place, dword at 24",
+                          "in place, 16-B piece rewritten", "in place, 32-B sector rewritten",
+                          "in place, 64-B sector rewritten", "in place, 128-B line rewritten"};
   printf("%u slots x %u B (%.3f GB), grid 2048 x 1024, dwordx4 nt loads, %u in flight\n", nslots, kSlot, nbytes / 1e9,
          D);
-  for (int m = 0; m < 6; ++m) {
+  for (int m = 0; m < 10; ++m) {
     std::sort(t[m].begin(), t[m].end());
     const float ms = t[m][4];
     printf("mode %d %-30s: %.4f ms  %.1f GB/s (slot bytes)  %+.1f %%\n", m, what[m], ms, nbytes / ms / 1e6,
