@@ -38,6 +38,24 @@ def main():
     summary = {"workload": wl, "kernel": kern[0]["Name"] if kern else None,
                "avg_ns": float(kern[0]["AverageNs"]) if kern else None,
                "calls": int(kern[0]["Calls"]) if kern else None, "counters": {}}
+    # avg_ns covers every traced dispatch, the 0.5 s prewarm at ramping clocks
+    # included; the bench's timed steps are the last `steps` dispatches
+    tr = os.path.join(src, "trace", "trace_kernel_trace.csv")
+    if os.path.exists(tr):
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr))
+             if KERNEL in r["Kernel_Name"]]
+        steps = 20
+        try:
+            for line in open(os.path.join(src, "bench_trace.log")):
+                if line.startswith("{"):
+                    steps = int(json.loads(line).get("steps", steps))
+        except (OSError, ValueError):
+            pass
+        if d:
+            last = d[-steps:]
+            summary["timed_steps_avg_ns"] = sum(last) / len(last)
+            summary["timed_steps"] = len(last)
+            summary["median_ns"] = sorted(d)[len(d) // 2]
     for i in range(1, 10):
         p = os.path.join(src, f"pmc{i}", "pmc_counter_collection.csv")
         if os.path.exists(p):
