@@ -1,10 +1,23 @@
-# A/B: ingress verdict kernel, qword lanes (product) vs the r1g dword lanes
+# A/B: ingress verdict / TX generate rows, per-wave buffer-descriptor loads
+# (product) against guarded global loads (LNX_PROF_INGRESS_UNROLL=1), after
+# the parity tests; three alternating bench runs of each.
+#   tools/prof/ingress_ab.sh TAG
 set -e
-O=gpurun_out/ingress_ab
+O=gpurun_out/ingress_ab_$1
 mkdir -p $O
-timeout -k 10 200 python -u -m pytest tests/test_ingress.py tests/test_rx_ring.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
-for i in 1 2; do
-  LNX_PROF_INGRESS_UNROLL=1 timeout -k 10 120 python -u bench.py --op ingress --no-cpu-baseline --steps 100 > $O/bench_nopf_$i.jsonl 2>> $O/bench.err
-  timeout -k 10 120 python -u bench.py --op ingress --no-cpu-baseline --steps 100 > $O/bench_pf_$i.jsonl 2>> $O/bench.err
+timeout -k 10 300 python -u -m pytest tests/test_ingress.py tests/test_rx_ring.py tests/test_tx_checksum.py -m gpu -x -q \
+  --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+tail -1 $O/tests.log
+for op in ingress tx_checksum; do
+  for i in 1 2 3; do
+    LNX_PROF_INGRESS_UNROLL=1 timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_global_$i.jsonl 2>> $O/bench.err
+    timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_buffer_$i.jsonl 2>> $O/bench.err
+  done
 done
-echo done
+python3 - $O <<'PY'
+import glob, json, sys
+o = sys.argv[1]
+for f in sorted(glob.glob(o + "/*.jsonl")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split("/")[-1], d["roofline"]["kernel_ms"], d["roofline"]["frac"])
+PY
