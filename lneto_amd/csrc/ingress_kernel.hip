@@ -84,7 +84,7 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
 // zeroed); lanes 0..7 of the row then store the 2-byte fields (IPv4 total
 // length / IPv6 payload length, header CRC, transport CRC, UDP length) and
 // `verdict` receives the status (0, or 18 / 15 with the frame untouched).
-template <int UNR, bool QW, bool GEN = false, bool BUF = true>
+template <int UNR, bool QW, bool GEN = false>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
@@ -111,69 +111,21 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const int32_t kfend = (int32_t)((L + mis + 3) >> 2);         // dwords touching the frame
 
     // ---- first batch: dwords kstart + p + 16u (QW: qwords qstart + p + 16u,
-    // qword Q = dwords 2Q, 2Q + 1); it also holds every header field
+    // qword Q = dwords 2Q, 2Q + 1); it also holds every header field.
+    // (Round 3 A/B: the same loads through one raw buffer descriptor per wave,
+    // out-of-range offsets in place of the guards, cost 8 more VGPRs, one
+    // wave per SIMD and 9 % of the time: 0.2696 against 0.2476 ms,
+    // profiles/r3n_ingress_buffer_loads_rejected.txt.)
     const uint2* base2 = reinterpret_cast<const uint2*>(base);
     const int32_t qstart = kstart >> 1, qfend = (kfend + 1) >> 1;
-    // QW: the wave's four frames through one raw buffer descriptor (base = the
-    // lowest frame start rounded down to 8, range = up to the highest frame
-    // end): a qword past the row's end takes an out-of-range offset and reads
-    // 0 with no traffic, one VALU select per load.  Guarded global loads cost
-    // an exec branch, two zeroing moves and a 64-bit address each
-    // (profiles/r3n_ingress_buffer_loads.txt).  A wave whose frames span 2 GiB
-    // or more keeps the global loads.
-    constexpr uint32_t kOOB = 0x80000000u;
-    bool bufw = false;
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(bytes), (short)0, 0, 0x00020000);
-    uint32_t rb = 0;  // byte offset of qword 0 of this row's frame (base2) in the descriptor
-    if constexpr (QW) {
-      auto rl64 = [](uint64_t v, int l) -> uint64_t {
-        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
-               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
-      };
-      // absolute addresses: the row's first qword, the end of its last qword
-      const uint64_t a0 = reinterpret_cast<uintptr_t>(base);
-      const uint64_t a1 = (reinterpret_cast<uintptr_t>(fr) + L + 7u) & ~7ull;
-      uint64_t wb = ~0ull, we = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint64_t sr = rl64(live && len64 ? a0 : ~0ull, 16 * r), er = rl64(live && len64 ? a1 : 0ull, 16 * r);
-        wb = sr < wb ? sr : wb;
-        we = er > we ? er : we;
-      }
-      bufw = BUF && we > wb && we - wb < (1ull << 31) - 4096u;
-      if (bufw) {
-        rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(wb), (short)0, (int)(we - wb), 0x00020000);
-        rb = live && len64 ? (uint32_t)(a0 - wb) : kOOB;
-      }
-    }
-    // a batch of UNR qwords q0 + 16u of the row (QW), zero at or past qe; the
-    // descriptor branch is taken once per batch (per load, hipcc interleaves
-    // the two forms and waits for every load before the next)
     uint32_t x[UNR];
     uint2 y[QW ? UNR : 1];
-    auto ld_batch = [&](int32_t q0, int32_t qe) {
-      if (bufw) {
-        const uint32_t vb = rb + 8u * (uint32_t)q0;
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          // (out of range + 128u is still out of range: the immediate offset folds)
-          const uint32_t vo = q0 + 16 * u < qe ? vb : kOOB;
-          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, vo + 128u * (uint32_t)u, 0, 0);
-          y[u] = make_uint2(v[0], v[1]);
-        }
+    for (int u = 0; u < UNR; ++u) {
+      if constexpr (QW) {
+        const int32_t q = qstart + (int32_t)p + 16 * u;
+        y[u] = L >= 14 && q < qfend ? base2[q] : make_uint2(0u, 0u);
       } else {
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          const int32_t q = q0 + 16 * u;
-          y[u] = q < qe ? base2[q] : make_uint2(0u, 0u);
-        }
-      }
-    };
-    if constexpr (QW) {
-      ld_batch(qstart + (int32_t)p, L >= 14 ? qfend : INT32_MIN);
-    } else {
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
         const int32_t k = kstart + (int32_t)p + 16 * u;
         x[u] = L >= 14 && k < kfend ? base[k] : 0u;
       }
@@ -419,7 +371,13 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       nit = __builtin_amdgcn_readfirstlane(nit);
       for (int32_t it = 0; it < nit; ++it) {
         const int32_t q0 = qstart + (int32_t)p + 16 * UNR * it;
-        if (!first) ld_batch(q0, qend);
+        if (!first) {
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) {
+            const int32_t q = q0 + 16 * u;
+            y[u] = q < qend ? base2[q] : make_uint2(0u, 0u);
+          }
+        }
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
 #pragma unroll
@@ -534,8 +492,7 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   const uint64_t cap = (uint64_t)num_cus * wg_per_cu;
   if (grid > cap) grid = cap;
   // profiling: LNX_PROF_INGRESS_UNROLL=8|16|24 selects the dword-lane form
-  // with that batch depth (24 = the r1g product), =1 the qword rows with
-  // guarded global loads
+  // with that batch depth (24 = the r1g product)
   static const int unr = [] {
     const char* e = getenv("LNX_PROF_INGRESS_UNROLL");
     return e ? atoi(e) : 0;
@@ -549,9 +506,6 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   else if (unr == kIngUnroll)
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnroll, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
                        off, n, flags, verdict, seg_len, trim);
-  else if (unr == 1)  // LNX_PROF_INGRESS_UNROLL=1: qword rows with guarded global loads (the r2 form, A/B)
-    hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, false, false>), dim3((unsigned)grid), dim3(kIngBlock), 0,
-                       stream, bytes, off, n, flags, verdict, seg_len, trim);
   else
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream,
                        bytes, off, n, flags, verdict, seg_len, trim);
