@@ -1,7 +1,9 @@
-# A/B: ingress verdict / TX generate rows, per-wave buffer-descriptor loads
-# (product) against guarded global loads (LNX_PROF_INGRESS_UNROLL=1), after
-# the parity tests; three alternating bench runs of each.
-#   tools/prof/ingress_ab.sh TAG
+# A/B: the ingress verdict / TX generate rows (product) against the form
+# LNX_PROF_INGRESS_UNROLL=U selects (default 24: the r1g dword lanes; r3n ran
+# it against a per-wave buffer-descriptor build, see
+# profiles/r3n_ingress_buffer_loads_rejected.txt), after the parity tests;
+# three alternating bench runs of each.
+#   tools/prof/ingress_ab.sh TAG [U]
 set -e
 O=gpurun_out/ingress_ab_$1
 mkdir -p $O
@@ -10,8 +12,8 @@ timeout -k 10 300 python -u -m pytest tests/test_ingress.py tests/test_rx_ring.p
 tail -1 $O/tests.log
 for op in ingress tx_checksum; do
   for i in 1 2 3; do
-    LNX_PROF_INGRESS_UNROLL=1 timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_global_$i.jsonl 2>> $O/bench.err
-    timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_buffer_$i.jsonl 2>> $O/bench.err
+    LNX_PROF_INGRESS_UNROLL=${2:-24} timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_alt_$i.jsonl 2>> $O/bench.err
+    timeout -k 10 120 python -u bench.py --op $op --no-cpu-baseline --steps 100 > $O/${op}_product_$i.jsonl 2>> $O/bench.err
   done
 done
 python3 - $O <<'PY'
