@@ -202,3 +202,21 @@ def test_egress_packets_matches_oracle(cuda, flags):
         assert np.array_equal(bufs[i][:offset], before[i][:offset])
         assert np.array_equal(bufs[i][offset + len(want):], before[i][offset + len(want):])
     assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+def test_ring_icmp_flag(cuda):
+    """IngressPackets with the ICMP clients attached (LNX_VERIFY_ICMP): ICMPv4 /
+    ICMPv6 frames with their FCS, echo and other types, short and corrupted
+    messages; the flag travels through the ring's stages to the verdict kernel."""
+    frames = [_with_fcs(f) for f in G.icmp_frames(seed=21, count=1200)]
+    flags = L.VERIFY_ICMP | L.VERIFY_EVIL_BIT
+    ring = L.RxRing(400, slot_cap=_cap_for(frames, 0), batch_slots=100, depth=3)
+    try:
+        ok, verdict = ring.ingress_packets(frames, offset=0, flags=flags)
+    finally:
+        ring.close()
+    want_v = np.array([O.ingress_verdict(f[:-4], flags) for f in frames], dtype=np.uint8)
+    assert ok.all()
+    assert set(want_v.tolist()) >= {0, O.ERR_BAD_CRC, O.ERR_PACKET_DROP, O.ERR_TRUNCATED_FRAME}
+    assert np.array_equal(verdict, want_v)

@@ -205,3 +205,10 @@ def test_gpu_tx_checksum_then_ingress_verify(cuda):
     offs[0::2], offs[1::2] = starts, ends
     v = L.ingress_verify_batch(d, torch.from_numpy(offs).to(cuda)).cpu().numpy()[0::2]
     assert int(v.max()) == 0, np.nonzero(v)[0][:10]
+    # with the ICMP clients attached: no generated ICMP message fails its sum
+    # (other ICMPv4 types than echo are dropped before the sum, as the client does)
+    vi = L.ingress_verify_batch(d, torch.from_numpy(offs).to(cuda), flags=L.VERIFY_ICMP).cpu().numpy()[0::2]
+    img = d.cpu().numpy()
+    want = [O.ingress_verdict(img[s:e].tobytes(), O.VERIFY_ICMP) for s, e in zip(starts, ends)]
+    assert vi.tolist() == want
+    assert O.ERR_BAD_CRC not in want
