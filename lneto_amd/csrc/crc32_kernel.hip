@@ -1513,9 +1513,12 @@ constexpr uint64_t kLineMean = 4096;
 // Lean line rows (lines_body) from kShortMean up to this mean frame length
 // (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
 constexpr uint64_t kLeanMean = 1600;
+#include "stream_rows.hpp"
+
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
-          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4, int NW4 = 1>
+          int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4, int NW4 = 1,
+          int STR = 0>
 __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
@@ -1549,6 +1552,14 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   const bool narrow = rl == 4;
   // whole-line windows: the RL = 32 image
   const bool line = rl == 32 || (rl == 16 && (MIDW == 2 || lean));
+  // streaming rows (stream_rows.hpp) for the narrow rows' frames in offsets
+  // mode, when the slice's bytes fit 31-bit buffer offsets from a line-aligned base
+  bool strm = STR != 0 && narrow && !SEG && MODE != CrcMode::kAppend;
+  if (strm) {
+    const uint64_t nb_ = ob1 > ob0 ? ob1 - ob0 : 0;
+    const uint64_t adj_ = (reinterpret_cast<uintptr_t>(bytes) + ob0) & 127u;
+    strm = nb_ + adj_ + 4096 < (1ull << 31);
+  }
   {
     // compact image (lds_layout.hpp): thread t expands U value t into its 32
     // bank replicas (128 contiguous bytes, eight 16-byte writes started at a
@@ -1558,7 +1569,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
     // (4-lane rows of four words per lane fold 16 virtual lanes: the RL = 16 image)
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          image_index(line ? 32 : (narrow && NW4 == 4) ? 16 : rl) * kCompactDwords;
+                          image_index(strm ? 8 : line ? 32 : (narrow && NW4 == 4) ? 16 : rl) * kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
     const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
@@ -1596,7 +1607,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
   // A range (a workgroup's slice of frames) is addressed through one buffer
   // descriptor whose base is 4-byte aligned (128-byte aligned for 32-lane
   // rows, whose windows run between lines): rel(x) = x - off[fb0] + adj.
-  const uint32_t amask = line ? 127u : (narrow && NW4 == 4) ? 15u : 3u;
+  const uint32_t amask = (line || strm) ? 127u : (narrow && NW4 == 4) ? 15u : 3u;
   struct Range {
     uint64_t f0, f1, o0, o1;
     bool fits;  // byte range within 31-bit buffer offsets
@@ -1653,6 +1664,14 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // chunks of the own slice from the LDS counter
     const WaveCtx cx = ctx_of(own);
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
+    if constexpr (STR != 0 && !SEG && MODE != CrcMode::kAppend) {
+      if (strm) {
+        L.p = lane & 7u, L.row = lane >> 3;
+        stream_body<MODE, VAR>(lds, L, cx);
+        if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
+        return;
+      }
+    }
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG, NW4, true, NSR4>(lds, L, cx);
@@ -1786,6 +1805,8 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 139: LNX_W4(0, 3, 2, 32, 1); break;
       case 140: LNX_W4(0, 5, 2, 32, 1); break;
 #undef LNX_W4
+      // streaming rows (stream_rows.hpp) for the narrow rows' frames, under the product dispatch
+      case 150: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
