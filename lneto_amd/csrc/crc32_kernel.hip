@@ -1807,6 +1807,9 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
 #undef LNX_W4
       // streaming rows (stream_rows.hpp) for the narrow rows' frames, under the product dispatch
       case 150: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
+      // its loads + chain only (no frame boundaries), loads only
+      case 151: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
+      case 152: LNX_LAUNCH(CrcMode::kCrc, 152, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

@@ -22,6 +22,21 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+template <int W> struct Vt;
+template <> struct Vt<4> { typedef uint32_t T; };
+template <> struct Vt<8> { typedef u32x2 T; };
+template <> struct Vt<16> { typedef u32x4 T; };
+template <int W>
+__device__ __forceinline__ typename Vt<W>::T ldv2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  if constexpr (W == 8) return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  if constexpr (W == 16) return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ uint32_t fold(uint32_t v) { return v; }
+__device__ __forceinline__ uint32_t fold(u32x2 v) { return v[0] ^ v[1]; }
+__device__ __forceinline__ uint32_t fold(u32x4 v) { return v[0] ^ v[1] ^ v[2] ^ v[3]; }
+
 template <int P>
 __device__ __forceinline__ u32x4 ldv(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, P);
@@ -146,6 +161,79 @@ __global__ void __launch_bounds__(1024) pat6(const uint8_t* __restrict__ base, u
   if (pad[(threadIdx.x + 1) & 1023] == 0x12345678u) out[0] = acc;
 }
 
+
+// Per-frame windows (each frame from its own aligned start, as the product's
+// rows) with the frame offsets prefetched 8 frames ahead in a register ring
+// (no dependent offset load on the critical path).  RL lanes x W bytes per row
+// step; CONTIG = 1: row r takes frames f0 + rK .. (contiguous, the shared line
+// comes back to the same row one step later); CONTIG = 0: row r takes frames
+// f0 + r, f0 + r + ROWS, ... (the product's interleave).
+template <int W, int RL, int D, int A, int CONTIG>
+__global__ void __launch_bounds__(1024) pat7(const uint8_t* __restrict__ base, uint32_t nbytes,
+                                             const uint32_t* __restrict__ off, const uint32_t* __restrict__ rowf,
+                                             uint32_t* out) {
+  __shared__ uint32_t pad[40960];
+  constexpr uint32_t ROWS = 64 / RL, RB = RL * W;
+  const uint32_t lane = threadIdx.x & 63, p = lane % RL, row = lane / RL;
+  const uint32_t gw = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const uint32_t w0 = rowf[gw * 8], w1 = rowf[gw * 8 + 8];
+  const uint32_t nfw = w1 - w0;
+  uint32_t f, f1, st;
+  if (CONTIG) {
+    f = w0 + (uint32_t)((uint64_t)nfw * row / ROWS), f1 = w0 + (uint32_t)((uint64_t)nfw * (row + 1) / ROWS), st = 1;
+  } else {
+    f = w0 + row, f1 = w1, st = ROWS;
+  }
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)off, (short)0, (int)0x7FFFFFF0, 0x00020000);
+  // offset ring: starts and ends of the next 8 frames
+  uint32_t ra[8], re[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t fi = f + i * st;
+    ra[i] = fi < f1 ? off[fi] : 0xFFFFF000u;
+    re[i] = fi < f1 ? off[fi + 1] : 0;
+  }
+  uint32_t a = ra[0] & ~(uint32_t)(A - 1), e = re[0];
+  bool live = f < f1;
+  if (!live) a = 0xFFFFF000u;
+  auto next = [&]() -> uint32_t {
+    const uint32_t o = a + p * W;
+    if (live) {
+      a += RB;
+      if (a >= e) {
+        f += st;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ra[i] = ra[i + 1], re[i] = re[i + 1];
+        const uint32_t fn = f + 7 * st;
+        ra[7] = __builtin_amdgcn_raw_buffer_load_b32(ro, fn < f1 ? fn * 4 : 0xFFFFF000u, 0, 0);
+        re[7] = __builtin_amdgcn_raw_buffer_load_b32(ro, fn < f1 ? fn * 4 + 4 : 0xFFFFF000u, 0, 0);
+        live = f < f1;
+        a = live ? (ra[0] & ~(uint32_t)(A - 1)) : 0xFFFFF000u;
+        e = re[0];
+      }
+    }
+    return o;
+  };
+  typename Vt<W>::T v[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) v[u] = ldv2<W>(r, next());
+  uint32_t acc = 0;
+  for (;;) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      acc ^= fold(v[u]);
+      v[u] = ldv2<W>(r, next());
+    }
+    if (!__builtin_amdgcn_ballot_w64(live)) break;
+  }
+#pragma unroll
+  for (int u = 0; u < D; ++u) acc ^= fold(v[u]);
+  pad[threadIdx.x] = acc;
+  __syncthreads();
+  if (pad[(threadIdx.x + 1) & 1023] == 0x12345678u) out[0] = acc;
+}
+
 template <typename F>
 float tm(F fn) {
   hipEvent_t a, b;
@@ -209,6 +297,18 @@ int main(int argc, char** argv) {
     float ms = tm([&] { pat6<D, H, P><<<256, 1024>>>(buf, nbytes + 4096, doff, drow, out); });            \
     printf("4-lane rows half=%d D=%2d pol=%d : %.4f ms %.1f GB/s of frame bytes\n", H, D, P, ms, nbytes / ms / 1e6); \
   }
+#define RUN7(W, RL, D, A, C)                                                                              \
+  {                                                                                                         \
+    float ms = tm([&] { pat7<W, RL, D, A, C><<<256, 1024>>>(buf, nbytes + 4096, doff, drow, out); });     \
+    printf("per-frame windows W=%2d RL=%2d D=%d align=%3d contig=%d : %.4f ms %.1f GB/s\n", W, RL, D, A, C, ms, nbytes / ms / 1e6); \
+  }
+  RUN7(4, 4, 16, 4, 0);
+  RUN7(4, 4, 16, 4, 1);
+  RUN7(16, 4, 8, 16, 0);
+  RUN7(16, 4, 8, 16, 1);
+  RUN7(16, 8, 8, 128, 0);
+  RUN7(16, 8, 8, 128, 1);
+  RUN7(8, 16, 8, 128, 1);
   RUN6(4, 1, 0);
   RUN6(4, 1, 2);
   RUN6(4, 0, 0);
