@@ -13,6 +13,10 @@
 //   7: in place, the whole 32-byte sector [1472, 1504) rewritten
 //   8: in place, the whole 64-byte sector [1472, 1536) rewritten
 //   9: in place, the whole 128-byte line [1408, 1536) rewritten
+//  10: in place at byte 1496, held in a register and stored after the
+//      thread's last read (writes deferred to the end of each thread's work)
+//  11: a separate launch storing the 4-byte results in place (the reads-only
+//      kernel's cost is mode 0; mode 3 + mode 11 = a compact array, then a scatter)
 // Not part of the product.  usage: scatter_write [nslots]
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -29,7 +33,12 @@ __global__ void __launch_bounds__(1024) rd(const u32x4* __restrict__ src, uint8_
                                            uint32_t nchunks) {
   const uint32_t nt = gridDim.x * blockDim.x;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t acc = 0;
+  uint32_t acc = 0, held_slot = 0xFFFFFFFFu, held = 0;
+  if constexpr (MODE == 11) {  // scatter only: slot i's result from the compact array
+    for (uint32_t s = i; s < nchunks / kChunks; s += nt)
+      *reinterpret_cast<uint32_t*>(data + (size_t)s * kSlot + 1496) = compact[s];
+    return;
+  }
   for (; i + (D - 1) * nt < nchunks; i += D * nt) {
     u32x4 v[D];
 #pragma unroll
@@ -48,6 +57,11 @@ __global__ void __launch_bounds__(1024) rd(const u32x4* __restrict__ src, uint8_
         }
       } else if constexpr (MODE == 3) {
         if (k == 1496 / 16) compact[slot] = acc;
+      } else if constexpr (MODE == 10) {
+        if (k == 1496 / 16) {
+          if (held_slot != 0xFFFFFFFFu) *reinterpret_cast<uint32_t*>(data + (size_t)held_slot * kSlot + 1496) = held;
+          held_slot = slot, held = acc;
+        }
       } else if constexpr (MODE == 5) {
         if (k == 1) *reinterpret_cast<uint32_t*>(data + (size_t)slot * kSlot + 24) = acc;
       } else if constexpr (MODE >= 6) {
@@ -61,6 +75,9 @@ __global__ void __launch_bounds__(1024) rd(const u32x4* __restrict__ src, uint8_
         }
       }
     }
+  }
+  if constexpr (MODE == 10) {
+    if (held_slot != 0xFFFFFFFFu) *reinterpret_cast<uint32_t*>(data + (size_t)held_slot * kSlot + 1496) = held;
   }
   if (acc == 0x9E3779B9u) compact[0] = acc;  // keeps the reads live in mode 0
 }
@@ -90,13 +107,15 @@ int main(int argc, char** argv) {
       case 7: rd<7><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
       case 8: rd<8><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
       case 9: rd<9><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 10: rd<10><<<g, blk>>>((const u32x4*)buf, buf, compact, nchunks); break;
+      case 11: rd<11><<<dim3(1024), dim3(1024)>>>((const u32x4*)buf, buf, compact, nchunks); break;
     }
   };
   for (int k = 0; k < 200; ++k) launch(0);
   (void)hipDeviceSynchronize();
-  std::vector<std::vector<float>> t(10);
+  std::vector<std::vector<float>> t(12);
   for (int r = 0; r < 9; ++r)
-    for (int m = 0; m < 10; ++m) {
+    for (int m = 0; m < 12; ++m) {
       (void)hipEventRecord(a);
       for (int k = 0; k < 10; ++k) launch(m);
       (void)hipEventRecord(b);
@@ -105,13 +124,14 @@ int main(int argc, char** argv) {
       (void)hipEventElapsedTime(&ms, a, b);
       t[m].push_back(ms / 10);
     }
-  const char* what[10] = {"reads only", "in place, dword at 1496", "in place, non-temporal dword",
+  const char* what[12] = {"reads only", "in place, dword at 1496", "in place, non-temporal dword",
                           "compact array (4 B per slot)", "in place, four byte stores", "in place, dword at 24",
                           "in place, 16-B piece rewritten", "in place, 32-B sector rewritten",
-                          "in place, 64-B sector rewritten", "in place, 128-B line rewritten"};
+                          "in place, 64-B sector rewritten", "in place, 128-B line rewritten",
+                          "in place, held to the end", "scatter launch alone"};
   printf("%u slots x %u B (%.3f GB), grid 2048 x 1024, dwordx4 nt loads, %u in flight\n", nslots, kSlot, nbytes / 1e9,
          D);
-  for (int m = 0; m < 10; ++m) {
+  for (int m = 0; m < 12; ++m) {
     std::sort(t[m].begin(), t[m].end());
     const float ms = t[m][4];
     printf("mode %d %-30s: %.4f ms  %.1f GB/s (slot bytes)  %+.1f %%\n", m, what[m], ms, nbytes / ms / 1e6,
