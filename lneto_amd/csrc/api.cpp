@@ -28,6 +28,8 @@ hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, co
                                  void* out, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
+hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
+                              uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
@@ -138,6 +140,16 @@ struct DeviceCtx {
   void* d_image = nullptr;
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
+  // Per-stream scratch of the two-launch TX append (the CRCs between its
+  // launches): calls on one stream run in order, so each stream reuses its
+  // buffer; it grows, after a sync of that stream, when a batch outgrows it.
+  struct Scratch {
+    hipStream_t stream;
+    void* p;
+    size_t cap;
+  };
+  std::mutex scratch_mu;
+  std::vector<Scratch> scratch;
 };
 
 constexpr int kMaxDevices = 64;
@@ -265,6 +277,31 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
   return LNX_OK;
 }
 
+// The calling device's scratch for `stream`, at least `bytes` long.
+static int stream_scratch(DeviceCtx* c, hipStream_t stream, size_t bytes, void** out) {
+  std::lock_guard<std::mutex> lk(c->scratch_mu);
+  DeviceCtx::Scratch* sc = nullptr;
+  for (auto& x : c->scratch)
+    if (x.stream == stream) sc = &x;
+  if (!sc) {
+    c->scratch.push_back({stream, nullptr, 0});
+    sc = &c->scratch.back();
+  }
+  if (sc->cap < bytes) {
+    hipError_t e;
+    if (sc->p) {  // the stream's earlier launches may still read the old buffer
+      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "hipStreamSynchronize(scratch)");
+      (void)hipFree(sc->p);
+      sc->p = nullptr, sc->cap = 0;
+    }
+    const size_t want = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+    if ((e = hipMalloc(&sc->p, want)) != hipSuccess) return hip_fail(e, "hipMalloc(scratch)");
+    sc->cap = want;
+  }
+  *out = sc->p;
+  return LNX_OK;
+}
+
 int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                        uint32_t* d_crc, void* stream) {
   if (n == 0) return LNX_OK;
@@ -286,9 +323,25 @@ int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   // one launch of the CRC kernel in its append mode: no scratch, no allocation
+  // (a compact CRC array plus a scatter launch measured the same, 0.331 ms:
+  // lnx__fcs_append_variant 200)
   const hipError_t e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, c->d_image, c->num_cus,
                                          static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel (append) launch");
+  return LNX_OK;
+}
+
+// TX append in two launches (A/B, lnx__fcs_append_variant 200): the segment-mode
+// CRC kernel into a compact per-stream scratch, then fcs_scatter_kernel.
+static int fcs_append_two_launch(DeviceCtx* c, uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n,
+                                 uint32_t capacity, uint8_t* d_status, hipStream_t s) {
+  uint32_t* scr = nullptr;
+  int st = stream_scratch(c, s, n * sizeof(uint32_t), reinterpret_cast<void**>(&scr));
+  if (st != LNX_OK) return st;
+  hipError_t e = launch_crc32_segments(d_bytes, d_start, d_len, n, scr, c->d_image, c->num_cus, s);
+  if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel (append: segments) launch");
+  e = launch_fcs_scatter(d_bytes, d_start, d_len, scr, n, capacity, d_status, c->num_cus, s);
+  if (e != hipSuccess) return hip_fail(e, "fcs_scatter_kernel launch");
   return LNX_OK;
 }
 
@@ -412,8 +465,12 @@ int lnx__fcs_append_variant(int var, uint8_t* d_bytes, const uint64_t* d_start, 
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
+  if (var == 200)  // two launches: CRCs into a compact scratch, then the scatter kernel
+    return fcs_append_two_launch(c, d_bytes, d_start, d_len, n, capacity, d_status, static_cast<hipStream_t>(stream));
+  // 100 (= 0): the one-launch append mode, the product; 4 / 7: its A/B forms
+  // (store at once / with the 64-byte sector)
   const hipError_t e = launch_fcs_append(d_bytes, d_start, d_len, n, capacity, d_status, c->d_image, c->num_cus,
-                                         static_cast<hipStream_t>(stream), var);
+                                         static_cast<hipStream_t>(stream), var == 100 ? 0 : var);
   if (e != hipSuccess) return hip_fail(e, "fcs append variant launch");
   return LNX_OK;
 }

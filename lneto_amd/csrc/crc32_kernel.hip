@@ -437,8 +437,9 @@ __device__ __forceinline__ uint32_t zero_advance(const char* lds, uint32_t x, ui
 // (store_held), so the ring's vmcnt waits do not wait on a store per slot.
 template <int RL, int IMGRL>
 __device__ __forceinline__ uint32_t append_pad(const char* lds, const Lanes& L, bool live, uint32_t n, uint32_t R,
-                                               uint8_t* e, uint32_t& k) {
-  k = live && n < kMinFrame ? kMinFrame - n : 0u;
+                                               uint8_t* e, uint32_t cap, uint32_t& k) {
+  // a runt that would outgrow its slot once padded is left untouched (status 6)
+  k = live && n < kMinFrame && kMinFrame + 4u <= cap ? kMinFrame - n : 0u;
   if (wave_any(k != 0u)) {
     const uint32_t z = zero_advance<RL, IMGRL>(lds, R, k, L);
     R = k ? z : R;
@@ -992,7 +993,7 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
       if constexpr (MODE == CrcMode::kAppend) {
         const bool lv = fin.last && fin.f != kNoFrame;
         if constexpr (kHold)
-          R = append_pad<RL, kImg>(lds, Lz, lv, n, R, cx.ap.data_base + fin.e, kpad);
+          R = append_pad<RL, kImg>(lds, Lz, lv, n, R, cx.ap.data_base + fin.e, cx.ap.cap, kpad);
         else  // VAR 4: the FCS, length and status stored at once (A/B)
           append_tail<RL, kImg>(lds, Lz, lv, n, R, cx.ap.data_base + fin.e, cx.ap.cap, cx.ap.lenw + fin.f,
                                 cx.ap.stat + fin.f);
@@ -1009,7 +1010,8 @@ __device__ __forceinline__ void rows_body(const char* lds, const Lanes& L, const
         hf = fin.f, hv = result_of<MODE>(n, crc);
         if constexpr (MODE == CrcMode::kAppend) {
           he = fin.e + kpad;
-          hpl = (uint64_t)n + kpad + 4u <= cx.ap.cap ? n + kpad + 4u : 0u;
+          const uint32_t kf = n < kMinFrame ? kMinFrame - n : 0u;  // the pad the frame needs
+          hpl = (uint64_t)n + kf + 4u <= cx.ap.cap ? n + kf + 4u : 0u;
         }
       }
       pc += fin.last ? 1u : 0u;
@@ -1406,7 +1408,7 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
                                          cx.ap.stat + fin.f);
       return;
     } else if constexpr (MODE == CrcMode::kAppend) {
-      R = append_pad<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, kpad);
+      R = append_pad<WL == 2 ? 16 : 32, 32>(lds, L, live, n, R, cx.ap.data_base + fin.e, cx.ap.cap, kpad);
     }
     const uint32_t crc = ~R;
     bool sec = false;  // kSector: this row's FCS went out with its sector
@@ -1434,7 +1436,8 @@ __device__ __forceinline__ void lines_body(const char* lds, const Lanes& L, cons
       hf = fin.f, hv = result_of<MODE>(n, crc);
       if constexpr (MODE == CrcMode::kAppend) {
         he = sec ? kFcsWritten : fin.e + kpad;
-        hpl = (uint64_t)n + kpad + 4u <= cx.ap.cap ? n + kpad + 4u : 0u;
+        const uint32_t kf = n < kMinFrame ? kMinFrame - n : 0u;  // the pad the frame needs
+        hpl = (uint64_t)n + kf + 4u <= cx.ap.cap ? n + kf + 4u : 0u;
       }
     }
     pc += live ? 1u : 0u;
@@ -1846,6 +1849,52 @@ hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* le
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var) {
   return launch_rows(var, CrcMode::kAppend, bytes, start, n, status, images, num_cus, stream, nullptr, len, capacity);
 }
+// TX FCS append, second launch (lnx_fcs_append_batch): frame i's CRC, taken
+// by the segment-mode CRC kernel into a compact array, goes into the frame's
+// slot here, with the runt padding, the new length and the status
+// (internet/stack-ethernet.go:200-214; oracle.fcs_append).  Stores in place
+// during the CRC kernel's read stream cost it about 30 %; the same 1 M stores
+// as a launch of their own take 16 us (tools/ubench/scatter_write.hip modes 1,
+// 3, 11).
+__global__ void __launch_bounds__(256) fcs_scatter_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start,
+                                                          uint32_t* __restrict__ len, const uint32_t* __restrict__ crc,
+                                                          uint64_t n, uint32_t cap, uint8_t* __restrict__ status) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t fl = len[i];
+    const uint32_t k = fl < kMinFrame ? kMinFrame - fl : 0u;  // zero pad of a runt
+    if ((uint64_t)fl + k + 4u > cap) {
+      status[i] = kErrShortBuffer;  // left untouched
+      continue;
+    }
+    uint8_t* fr = bytes + start[i];
+    uint32_t c = crc[i];
+    if (k) {  // CRC of the padded frame: the register advanced over k zero bytes
+      uint32_t r = ~c;
+      for (uint32_t b = 0; b < 8u * k; ++b) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
+      c = ~r;
+      for (uint32_t j = 0; j < k; ++j) fr[fl + j] = 0;
+    }
+    uint8_t* q = fr + fl + k;
+    if ((reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+      *reinterpret_cast<uint32_t*>(q) = c;  // LE: the FCS byte order
+    } else {
+      q[0] = (uint8_t)c, q[1] = (uint8_t)(c >> 8), q[2] = (uint8_t)(c >> 16), q[3] = (uint8_t)(c >> 24);
+    }
+    len[i] = fl + k + 4u;
+    status[i] = 0;
+  }
+}
+hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
+                              uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t grid = (n + 255) / 256;
+  const uint64_t gmax = (uint64_t)num_cus * 16;
+  if (grid > gmax) grid = gmax;
+  hipLaunchKernelGGL(fcs_scatter_kernel, dim3((unsigned)grid), dim3(256), 0, stream, bytes, start, len, crc, n,
+                     capacity, status);
+  return hipGetLastError();
+}
+
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {
   const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;

@@ -115,11 +115,14 @@ def test_gpu_crc32_segments(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", [4, 7])
+@pytest.mark.parametrize("var", [4, 7, 100, 200])
 @pytest.mark.parametrize("cap,base", [(1536, 0), (1536, 1), (1600, 5)])
 def test_gpu_fcs_append_ab_variants(cuda, var, cap, base):
     """The append A/B variants (lnx__fcs_append_variant) write what the product
-    writes: 4 = FCS, length and status stored as each frame finishes; 7 = the
+    writes: 200 = two launches (CRC kernel into a compact scratch, then the
+    scatter kernel); 100 = the one-launch append mode, the product (FCS,
+    length and status held and flushed by the CRC kernel); 4 = that mode
+    storing as each frame finishes; 7 = the
     FCS written with its whole 64-byte sector (bytes after it rewritten as
     loaded; frames whose FCS straddles a sector, the range's last frame and
     sectors past the slot take the held path)."""
@@ -151,3 +154,30 @@ def test_gpu_fcs_append_ab_variants(cuda, var, cap, base):
         assert int(status[i]) == stw and int(got_len[i]) == len(want), i
     diff = np.nonzero(got != want_img)[0]
     assert diff.size == 0, [(int(x), int((x - base) // cap)) for x in diff[:10]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [63, 64, 65, 100])
+def test_gpu_fcs_append_small_capacity(cuda, cap):
+    """Runts pad to 60 bytes: with a capacity under 64 they do not fit and stay
+    untouched (status ErrShortBuffer, internet/stack-ethernet.go:170-179 per
+    frame); frames of every length 0..cap around the limit."""
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(cap)
+    lens = np.tile(np.arange(0, cap + 1), 3).astype(np.int64)
+    n = len(lens)
+    data = rng.integers(0, 256, size=n * cap + 8, dtype=np.uint8)
+    starts = np.arange(n, dtype=np.int64) * cap
+    d = torch.from_numpy(data.copy()).to(cuda)
+    dl = torch.from_numpy(lens.astype(np.int32)).to(cuda)
+    status = L.fcs_append_batch(d, torch.from_numpy(starts).to(cuda), dl, cap).cpu().numpy()
+    got, got_len = d.cpu().numpy(), dl.cpu().numpy()
+    want_img = data.copy()
+    for i in range(n):
+        s = int(starts[i])
+        want, stw = O.fcs_append(data[s:s + int(lens[i])].tobytes(), cap)
+        want_img[s:s + len(want)] = np.frombuffer(want, dtype=np.uint8)
+        assert int(status[i]) == stw, (i, int(lens[i]))
+        assert int(got_len[i]) == (len(want) if stw == 0 else int(lens[i])), (i, int(lens[i]))
+    assert np.array_equal(got, want_img)

@@ -1,4 +1,5 @@
-"""A/B of the TX FCS append variants (lnx__fcs_append_variant: 0 = product,
+"""A/B of the TX FCS append variants (lnx__fcs_append_variant: 0 / 100 = the product, one launch,
+200 = two launches (CRC kernel into a compact scratch, then a scatter kernel),
 results held and flushed; 4 = FCS / length / status stored as each frame
 finishes; 7 = the FCS written with its whole 64-byte sector; -1 = no append: lnx_crc32_segments
 over the same frames, the body's cost alone) on bench.py's fcs_append workload: 1 M frames of 1496 B in 1536-B
