@@ -60,11 +60,13 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
   return img;
 }
 
-// The LDS image of the streaming rows (stream_rows.hpp): U = Z_4 (the chain's
-// dword step), F column n = Z_{-4n} (n = 0..31), then Z_116 byte tables, Z_c
-// (c = 0..3) and Z_{128-4k} (k = 0..4) nibble tables by row lane, the
-// constants Z_{128-j}(0xFFFFFFFF) and the Z_1 byte table.
-std::vector<uint32_t> build_stream_image() {
+// The LDS image of the streaming rows (stream_rows.hpp) with row steps of SB
+// bytes (128: 8-lane rows, 64: 4-lane rows): U = Z_4 (the chain's dword step),
+// F column n = Z_{-4n} (n = 0..31), then the Z_{SB-12} byte tables (the skip
+// over the other lanes' pieces, at kSZ116), Z_c (c = 0..3) and Z_{SB-4k}
+// (k = 0..4) nibble tables by row lane, the constants Z_{SB-j}(0xFFFFFFFF) and
+// the Z_1 byte table.
+std::vector<uint32_t> build_stream_image(int64_t sb) {
   std::vector<uint32_t> img(kLdsDwords, 0);
   for (uint32_t m = 0; m < 4; ++m)
     for (uint32_t e = 0; e < 256; ++e) {
@@ -75,15 +77,15 @@ std::vector<uint32_t> build_stream_image() {
     for (uint32_t i = 0; i < 8; ++i)
       for (uint32_t v = 0; v < 16; ++v) img[f_addr(c, i, v) / 4] = zshift_bytes(v << (4 * i), -4 * (int64_t)c);
   for (uint32_t m = 0; m < 4; ++m)
-    for (uint32_t e = 0; e < 256; ++e) img[(kSZ116 + 1024 * m + 4 * e) / 4] = zshift_bytes(e << (8 * m), 116);
+    for (uint32_t e = 0; e < 256; ++e) img[(kSZ116 + 1024 * m + 4 * e) / 4] = zshift_bytes(e << (8 * m), sb - 12);
   for (uint32_t c = 0; c < 4; ++c)
     for (uint32_t p = 0; p < 8; ++p)
       for (uint32_t v = 0; v < 16; ++v) img[kSTc / 4 + (c * 8 + p) * 16 + v] = zshift_bytes(v << (4 * p), c);
   for (uint32_t k = 0; k < 5; ++k)
     for (uint32_t p = 0; p < 8; ++p)
       for (uint32_t v = 0; v < 16; ++v)
-        img[kSG / 4 + (k * 8 + p) * 16 + v] = zshift_bytes(v << (4 * p), 128 - 4 * (int64_t)k);
-  for (uint32_t j = 0; j < 16; ++j) img[kSK / 4 + j] = zshift_bytes(0xFFFFFFFFu, 128 - (int64_t)j);
+        img[kSG / 4 + (k * 8 + p) * 16 + v] = zshift_bytes(v << (4 * p), sb - 4 * (int64_t)k);
+  for (uint32_t j = 0; j < 16; ++j) img[kSK / 4 + j] = zshift_bytes(0xFFFFFFFFu, sb - (int64_t)j);
   for (uint32_t e = 0; e < 256; ++e) img[kST1 / 4 + e] = zshift_bytes(e, 1);
   return img;
 }
@@ -165,12 +167,13 @@ std::vector<uint32_t> compact_image(const std::vector<uint32_t>& full) {
   return c;
 }
 
-// The compact images back to back: [RL = 16][RL = 4][RL = 32][stream] (lds_layout.hpp image_index).
+// The compact images back to back: [RL = 16][RL = 4][RL = 32][stream][stream64] (lds_layout.hpp image_index).
 const std::vector<uint32_t>& host_image() {
   static const std::vector<uint32_t> img = [] {
     std::vector<uint32_t> all;
-    for (uint32_t rl : {16u, 4u, 32u, 8u}) {
-      const std::vector<uint32_t> im = compact_image(rl == 8 ? build_stream_image() : build_lds_image(rl));
+    for (uint32_t rl : {16u, 4u, 32u, 8u, 9u}) {  // 8, 9: the stream images (128- and 64-byte row steps)
+      const std::vector<uint32_t> im =
+          compact_image(rl == 8 ? build_stream_image(128) : rl == 9 ? build_stream_image(64) : build_lds_image(rl));
       all.insert(all.end(), im.begin(), im.end());
     }
     return all;

@@ -1572,7 +1572,8 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
     // (4-lane rows of four words per lane fold 16 virtual lanes: the RL = 16 image)
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          image_index(strm ? 8 : line ? 32 : (narrow && NW4 == 4) ? 16 : rl) * kCompactDwords;
+                          image_index(strm ? (STR == 2 ? 9 : 8) : line ? 32 : (narrow && NW4 == 4) ? 16 : rl) *
+                              kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
     const uint4* tail = reinterpret_cast<const uint4*>(img + kCompactUDwords);
@@ -1669,8 +1670,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
     if constexpr (STR != 0 && !SEG && MODE != CrcMode::kAppend) {
       if (strm) {
-        L.p = lane & 7u, L.row = lane >> 3;
-        stream_body<MODE, VAR>(lds, L, cx);
+        constexpr int RLS = STR == 2 ? 4 : 8;
+        L.p = lane & (RLS - 1u), L.row = lane / RLS;
+        stream_body<MODE, VAR, RLS>(lds, L, cx);
         if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
         return;
       }
@@ -1813,6 +1815,10 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       // its loads + chain only (no frame boundaries), loads only
       case 151: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
       case 152: LNX_LAUNCH(CrcMode::kCrc, 152, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
+      // the same on 4-lane rows (64-byte row steps, at most one boundary per step): full, loads + chain, loads
+      case 153: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
+      case 154: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
+      case 155: LNX_LAUNCH(CrcMode::kCrc, 152, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

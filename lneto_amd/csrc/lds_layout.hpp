@@ -51,10 +51,10 @@ constexpr uint32_t kLdsDwords = kLdsBytes / 4;
 constexpr uint32_t kFBase = 131072;                // start of the F region
 constexpr uint32_t kTBase = 147456;                // start of the T region
 constexpr uint32_t kCtrBase = 159744;              // frame-chunk counter (one dword)
-constexpr int kImageCount = 4;                     // images: [0] RL = 16, [1] RL = 4, [2] RL = 32, [3] stream
+constexpr int kImageCount = 5;  // images: [0] RL = 16, [1] RL = 4, [2] RL = 32, [3] stream, [4] stream64
 // the streaming rows' image (stream_rows.hpp): U = Z_4, F column n = Z_{-4n},
 // then the Z_116 / Z_c / Z_{128-4k} / Z_1 tables at these byte addresses
-constexpr uint32_t kSZ116 = 147456;  // Z_116 byte tables: entry (m, e) at 1024m + 4e
+constexpr uint32_t kSZ116 = 147456;  // Z_{SB-12} byte tables (Z_116 / Z_52): entry (m, e) at 1024m + 4e
 constexpr uint32_t kSTc = 151552;    // Z_c, c = 0..3, nibble p of the row: dword ((c*8 + p)*16 + v)
 constexpr uint32_t kSG = 153600;     // Z_{128-4k}, k = 0..4, nibble p: dword ((k*8 + p)*16 + v)
 constexpr uint32_t kSK = 156160;     // Z_{128-j}(0xFFFFFFFF), j = 0..15
@@ -70,7 +70,8 @@ constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // 
   return kTBase + ((48u * h + 16u * (t - 1) + v) << 7) + (c << 2);
 }
 static_assert(t_addr(31, 1, 3, 15) < kCtrBase, "T region overlaps the counter");
-constexpr int image_index(int rl) { return rl == 16 ? 0 : rl == 4 ? 1 : rl == 8 ? 3 : 2; }
+// (8 and 9: the streaming rows' images with 128- and 64-byte row steps)
+constexpr int image_index(int rl) { return rl == 16 ? 0 : rl == 4 ? 1 : rl == 8 ? 3 : rl == 9 ? 4 : 2; }
 
 // Compact image in HBM (what a workgroup reads at start): the 1024 distinct U
 // values U_m[e] at dword 256m + e, then the [kFBase, kLdsBytes) tail of the

@@ -53,38 +53,59 @@ __device__ __forceinline__ uint32_t z1(const char* lds, uint32_t x) {
   return lds_rd(lds, kST1 + ((x & 0xFFu) << 2)) ^ (x >> 8);
 }
 
-template <CrcMode MODE, int VAR, int D = 4>
+// XOR over the RLS lanes of a row
+template <int RLS>
+__device__ __forceinline__ uint32_t rowx(uint32_t v) {
+  if constexpr (RLS == 8) return row8_xor(v);
+  v = dpp_xor<kQuadX1>(v);
+  return dpp_xor<kQuadX2>(v);
+}
+
+// RLS: lanes per row (8: one 128-byte line per row step, the stream image;
+// 4: a 64-byte half line, the stream64 image).  With 4-lane rows a frame of
+// at least 64 bytes ends at most once per row step, so a step takes one
+// boundary pass where 8-lane rows take up to two.
+template <CrcMode MODE, int VAR, int RLS = 8, int D = 4>
 __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, const WaveCtx& cx) {
   static_assert(MODE != CrcMode::kAppend, "offsets mode only");
-  const uint32_t p = L.p;  // lane of the row, 0..7
+  static_assert(RLS == 8 || RLS == 4, "row width");
+  constexpr uint32_t SB = 16u * RLS;                  // bytes per row step
+  constexpr uint32_t kRowLog = RLS == 8 ? 7 : 8;      // log2(rows per workgroup)
+  constexpr int OPL = 8 / RLS;                        // offsets per lane in an 8-event block
+  const uint32_t p = L.p;  // lane of the row
   const uint32_t bu0 = L.bu0, bu1 = L.bu1;
   const uint32_t nfb = cx.nfb, o0_lo = cx.o0_lo, adj = cx.adj;
   const __amdgpu_buffer_rsrc_t data_rsrc = cx.data_rsrc, off_rsrc = cx.off_rsrc, out_rsrc = cx.out_rsrc;
   auto rel = [&](uint32_t x_lo) -> uint32_t { return x_lo - o0_lo + adj; };
 
   // ---- the row's frames: [fr0, fr0 + m) of the range, events 0..m at off[fr0 + k]
-  const uint32_t jrow = (threadIdx.x >> 3);  // 0..127
-  const uint32_t fr0 = (uint32_t)(((uint64_t)jrow * nfb) >> 7), fr1 = (uint32_t)(((uint64_t)(jrow + 1) * nfb) >> 7);
+  const uint32_t jrow = threadIdx.x / RLS;
+  const uint32_t fr0 = (uint32_t)(((uint64_t)jrow * nfb) >> kRowLog),
+                 fr1 = (uint32_t)(((uint64_t)(jrow + 1) * nfb) >> kRowLog);
   const uint32_t m = fr1 - fr0;
   // first two offset blocks and the last event, synchronously
   auto ld_off = [&](uint32_t k) -> uint32_t {  // low dword of off[fr0 + k], k <= m; junk otherwise
     return __builtin_amdgcn_raw_buffer_load_b32(off_rsrc, k <= m ? (fr0 + k) * 8u : kOOB, 0, 0);
   };
-  uint32_t A = rel(ld_off(p)), B = rel(ld_off(8 + p));
+  // lane p holds events kb + p + RLS*i of the block in A[i] (the next block in B)
+  uint32_t A[OPL], B[OPL];
+#pragma unroll
+  for (int i = 0; i < OPL; ++i) A[i] = rel(ld_off(p + RLS * i)), B[i] = rel(ld_off(8 + p + RLS * i));
   const uint32_t xm = rel(__builtin_amdgcn_raw_buffer_load_b32(off_rsrc, fr1 * 8u, 0, 0));
   uint32_t kb = 0;             // event index of A's lane 0
   bool hasB = m >= 8;          // B holds events kb + 8 ..
   bool reqd = false;           // B's block requested, arriving in ob[reqs]
   uint32_t reqs = 0;
-  const uint32_t rowbase = (threadIdx.x & 63u) & ~7u;
+  const uint32_t rowbase = (threadIdx.x & 63u) & ~(RLS - 1u);
   auto pick = [&](uint32_t j) -> uint32_t {  // event kb + j, j < 16: from A (j < 8) or B
-    const uint32_t v = j < 8u ? A : B;
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rowbase + (j & 7u)) << 2), (int)v);
+    uint32_t v = j < 8u ? A[0] : B[0];
+    if constexpr (OPL == 2) v = ((j >> 2) & 1u) ? (j < 8u ? A[1] : B[1]) : v;
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rowbase + (j & (RLS - 1u))) << 2), (int)v);
   };
   uint32_t k = 0;                         // next event
   uint32_t x = pick(0);                   // its position
-  uint32_t Lr = x & ~127u;                // the row's current line
-  const uint32_t Lend = xm & ~127u;       // its last line
+  uint32_t Lr = x & ~(SB - 1u);           // the row's current line (row step)
+  const uint32_t Lend = xm & ~(SB - 1u);  // its last one
   uint32_t xs = x;                        // the previous event (verify: frame length)
   uint32_t r = 0;                         // the lane's chain register
   uint32_t P = 0, xprev = 0, pprev = 0xFFu;  // same-piece events (frames < 16 B)
@@ -98,13 +119,17 @@ __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, con
   // register above the ring's wait (tools/prof/audit_ring.py).
   constexpr int R = D + 1;
   u32x4 w[R];
-  uint32_t ob[R];
+  uint32_t ob[R][OPL];
   auto issue = [&](int s, uint32_t line, bool req, uint32_t kreq) {
     const uint32_t vl = line <= Lend ? line + 16u * p : kOOB;
     const uint32_t vo = req && kreq + p <= m ? (fr0 + kreq + p) * 8u : kOOB;
     asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %2, %4, 0 offen\n\tbuffer_load_dword %1, %3, %5, 0 offen"
-                 : "=&v"(w[s]), "=&v"(ob[s])
+                 : "=&v"(w[s]), "=&v"(ob[s][0])
                  : "v"(vl), "v"(vo), "s"(data_rsrc), "s"(off_rsrc));
+    if constexpr (OPL == 2) {
+      const uint32_t vo1 = req && kreq + p + RLS <= m ? (fr0 + kreq + p + RLS) * 8u : kOOB;
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=&v"(ob[s][1]) : "v"(vo1), "s"(off_rsrc));
+    }
   };
   auto store_held = [&]() {
     const uint32_t a = p < hc ? (MODE == CrcMode::kCrc ? hf * 4u : hf) : kOOB;
@@ -116,43 +141,47 @@ __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, con
   };
 #pragma unroll
   for (int s = 0; s < D; ++s) {
-    issue(s, Lr + 128u * s, false, 0);
+    issue(s, Lr + SB * s, false, 0);
     asm volatile("buffer_store_dword %0, %1, %2, 0 offen" ::"v"(0u), "v"(kOOB), "s"(out_rsrc) : "memory");
   }
 
-  auto pending = [&]() -> bool { return k <= m && x < Lr + 128u; };
+  auto pending = [&]() -> bool { return k <= m && x < Lr + SB; };
   // one event per row: the row's next frame boundary, if it lies in this line
   auto event = [&](const u32x4& wv, uint32_t y0, uint32_t y1, uint32_t y2, uint32_t y3, uint32_t& ra) {
     {
       const bool ev = pending();
-      const uint32_t rl = x - Lr;  // 0..127 where ev
-      const uint32_t pe = (rl >> 4) & 7u, ke = (rl >> 2) & 3u, c = rl & 3u;
+      const uint32_t rl = x - Lr;  // 0..SB-1 where ev
+      const uint32_t pe = (rl >> 4) & (RLS - 1u), ke = (rl >> 2) & 3u, c = rl & 3u;
       // the lane's value and F column
       const uint32_t yk = ke == 0 ? y0 : ke == 1 ? y1 : ke == 2 ? y2 : y3;
       const uint32_t wk = ke == 0 ? wv[0] : ke == 1 ? wv[1] : ke == 2 ? wv[2] : wv[3];
       const uint32_t hm = (uint32_t)(0xFFFFFFFFull << (8 * c));
       const uint32_t E = yk ^ (wk & hm);
       const uint32_t v = p == pe ? E : (p < pe ? ra : r);
-      const uint32_t n = p == pe ? 0u : 4u * ((p - pe) & 7u) - ke;
+      const uint32_t n = p == pe ? 0u : 4u * ((p - pe) & (RLS - 1u)) - ke;
       uint32_t O = f_step(lds, v, kFBase | (n << 2));
-      O = row8_xor(O);
-      // S = Z_c(O) and the injection's Z_{128-4k}(O), nibble p of O on lane p
-      const uint32_t nib = (O >> (4 * p)) & 15u;
-      uint32_t S = lds_rd(lds, kSTc + (((c * 8u + p) * 16u + nib) << 2));
-      uint32_t G = lds_rd(lds, kSG + (((ke * 8u + p) * 16u + nib) << 2));
-      S = row8_xor(S);
-      G = row8_xor(G) ^ lds_rd(lds, kSK + ((rl & 15u) << 2));
+      O = rowx<RLS>(O);
+      // S = Z_c(O) and the injection's Z_{SB-4k}(O): nibble p (and p + 4 on
+      // 4-lane rows) of O on lane p
+      auto nibs = [&](uint32_t base, uint32_t sel, uint32_t y) -> uint32_t {
+        uint32_t t = lds_rd(lds, base + (((sel * 8u + p) * 16u + ((y >> (4 * p)) & 15u)) << 2));
+        if constexpr (RLS == 4)
+          t ^= lds_rd(lds, base + (((sel * 8u + p + 4u) * 16u + ((y >> (4 * p + 16)) & 15u)) << 2));
+        return t;
+      };
+      uint32_t S = rowx<RLS>(nibs(kSTc, c, O));
+      uint32_t G = rowx<RLS>(nibs(kSG, ke, O)) ^ lds_rd(lds, kSK + ((rl & 15u) << 2));
       const bool same = pe == pprev;
       if (wave_any(ev && same)) {  // slow path: an earlier event of this row in the same lane piece
         if (ev && same) {          // (row-uniform: the row's 8 lanes together)
           uint32_t q = P;          // the piece's injections, moved from xprev to x
           for (uint32_t i = 0; i < x - xprev; ++i) q = z1(lds, q);
           S ^= q;
-          // G = Z_{128 - (rl & 15)}(~S) = Z_{128 - 4(ke + [c > 0])}(Z_{(4 - c) & 3}(~S))
+          // G = Z_{SB - (rl & 15)}(~S) = Z_{SB - 4(ke + [c > 0])}(Z_{(4 - c) & 3}(~S))
           uint32_t u = ~S;
           for (uint32_t i = 0; i < ((4u - c) & 3u); ++i) u = z1(lds, u);
           const uint32_t kk = ke + (c != 0u ? 1u : 0u);
-          G = row8_xor(lds_rd(lds, kSG + (((kk * 8u + p) * 16u + ((u >> (4 * p)) & 15u)) << 2)));
+          G = rowx<RLS>(nibs(kSG, kk, u));
           P = q;
         }
       }
@@ -172,24 +201,38 @@ __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, con
       if (wave_any(adv && !hasB)) {  // slow path: the next block is not here yet: load it now
         // (a request in flight is dropped: its set is not read on this path, so
         // hipcc keeps no copy of an outstanding ring register here)
-        const uint32_t nb = rel(ld_off(kb + 8u + p));
-        if (adv && !hasB) B = nb, reqd = false, hasB = true;
+        uint32_t nb[OPL];
+#pragma unroll
+        for (int i = 0; i < OPL; ++i) nb[i] = rel(ld_off(kb + 8u + p + RLS * i));
+        if (adv && !hasB) {
+#pragma unroll
+          for (int i = 0; i < OPL; ++i) B[i] = nb[i];
+          reqd = false, hasB = true;
+        }
       }
-      if (adv) A = B, kb += 8u, hasB = false;
+      if (adv) {
+#pragma unroll
+        for (int i = 0; i < OPL; ++i) A[i] = B[i];
+        kb += 8u, hasB = false;
+      }
       const uint32_t xn = pick(k - kb);
       if (ev) x = xn;
       if (wave_any(hc >= 2u && pending())) store_held();  // a third result in this line: flush (extra VMEM)
     }
   };
-  // Two events per row and line are the most frames of >= 64 bytes give;
-  // unrolled, so the common path has no loop (whose phi copies cost ~16 VALU
-  // an iteration); more (shorter frames) loop.
+  // Frames of >= 64 bytes end at most twice in a 128-byte row step and once
+  // in a 64-byte one: those passes are unrolled, so the common path has no
+  // loop (whose phi copies cost ~16 VALU an iteration); more (shorter frames) loop.
   auto event_loop = [&](const u32x4& wv, uint32_t y0, uint32_t y1, uint32_t y2, uint32_t y3, uint32_t& ra) {
     pprev = 0xFFu;
     if (wave_any(pending())) {
       event(wv, y0, y1, y2, y3, ra);
-      if (wave_any(pending())) {
-        event(wv, y0, y1, y2, y3, ra);
+      if constexpr (RLS == 8) {
+        if (wave_any(pending())) {
+          event(wv, y0, y1, y2, y3, ra);
+          while (wave_any(pending())) event(wv, y0, y1, y2, y3, ra);
+        }
+      } else {
         while (wave_any(pending())) event(wv, y0, y1, y2, y3, ra);
       }
     }
@@ -200,19 +243,28 @@ __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, con
 #pragma unroll
     for (int s = 0; s < R; ++s) {
       // set s holds line Lr
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * D - 2));
-      asm volatile("" : "+v"(w[s]), "+v"(ob[s]));
+      // loads younger than set s's: the store of its step, then D - 1 steps of
+      // (line, OPL offsets, store)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(1 + (2 + OPL) * (D - 1)));
+      asm volatile("" : "+v"(w[s]), "+v"(ob[s][0]));
+      if constexpr (OPL == 2) asm volatile("" : "+v"(ob[s][1]));
       const u32x4 wv = w[s];
       {
         const bool arr = reqd && reqs == (uint32_t)s;
-        const uint32_t bo = rel(ob[s]);
-        if (arr) B = bo, hasB = true, reqd = false;
+        uint32_t bo[OPL];
+#pragma unroll
+        for (int i = 0; i < OPL; ++i) bo[i] = rel(ob[s][i]);
+        if (arr) {
+#pragma unroll
+          for (int i = 0; i < OPL; ++i) B[i] = bo[i];
+          hasB = true, reqd = false;
+        }
       }
       // next request: B free, a block after it exists
       const bool req = !hasB && !reqd && kb + 8u <= m;
       const uint32_t kreq = kb + 8u;
       const int sn = (s + D) % R;  // the set step t - 1 used
-      issue(sn, Lr + 128u * D, req, kreq);
+      issue(sn, Lr + SB * D, req, kreq);
       if (req) reqd = true, reqs = (uint32_t)sn;
       // the fold
       uint32_t ra;
@@ -227,7 +279,7 @@ __device__ __forceinline__ void stream_body(const char* lds, const Lanes& L, con
         if constexpr (VAR != 151) event_loop(wv, y0, y1, y2, y3, ra);  // 151 (profiling): loads + chain only
       }
       r = ra;
-      Lr += 128u;
+      Lr += SB;
       if (Lr > Lend) k = m + 1u;  // past the row's last line (a bound every wave reaches)
       store_held();
       live = wave_any(k <= m);

@@ -79,13 +79,12 @@ def lomask(c: int) -> int:
     return (1 << (8 * c)) - 1
 
 
-RL = 8
-LINE = 128
-
-
-def stream_row(data: bytes, events: list[int]) -> list[int]:
+def stream_row(data: bytes, events: list[int], RL: int = 8) -> list[int]:
     """CRCs of the frames [events[i], events[i+1]) of one row, by the streaming
-    schedule.  data: the whole buffer (reads past its end are 0)."""
+    schedule with RL lanes per row (row steps of LINE = 16 RL bytes: 8 lanes,
+    one 128-byte line; 4 lanes, a 64-byte half line).  data: the whole buffer
+    (reads past its end are 0)."""
+    LINE = 16 * RL
     m = len(events) - 1
     out = []
     if m < 0:
@@ -109,7 +108,7 @@ def stream_row(data: bytes, events: list[int]) -> list[int]:
             y[p][1] = Zt(4, y[p][0]) ^ w[p][1]
             y[p][2] = Zt(4, y[p][1]) ^ w[p][2]
             y[p][3] = Zt(4, y[p][2]) ^ w[p][3]
-            ra[p] = Zt(116, y[p][3])
+            ra[p] = Zt(LINE - 12, y[p][3])
         piece_prev = -1  # lane piece of the previous event in this line
         x_prev = 0
         P = 0
@@ -120,7 +119,7 @@ def stream_row(data: bytes, events: list[int]) -> list[int]:
             O = 0
             for p in range(RL):
                 if p < pe:
-                    v, n = ra[p], 4 * ((p - pe) & 7) - ke
+                    v, n = ra[p], 4 * ((p - pe) % RL) - ke
                 elif p > pe:
                     v, n = r[p], 4 * (p - pe) - ke
                 else:
@@ -148,7 +147,7 @@ def stream_row(data: bytes, events: list[int]) -> list[int]:
     return out
 
 
-def check(frames: list[bytes], lead: int = 0) -> None:
+def check(frames: list[bytes], lead: int = 0, RL: int = 8) -> None:
     buf = bytes(range(256)) * ((lead + 255) // 256)
     data = bytearray(buf[:lead])
     ev = [lead]
@@ -156,7 +155,7 @@ def check(frames: list[bytes], lead: int = 0) -> None:
         data += f
         ev.append(len(data))
     data += bytes(range(7)) * 40  # junk after the run
-    got = stream_row(bytes(data), ev)
+    got = stream_row(bytes(data), ev, RL)
     want = [zlib.crc32(f) for f in frames]
     assert got == want, (got, want)
 
@@ -169,5 +168,5 @@ if __name__ == "__main__":
         lens = [rnd.choice([0, 1, 2, 3, 4, 5, 7, 15, 16, 17, 31, 63, 64, 65, 100, 127, 128, 129, 200, 1500])
                 for _ in range(rnd.randint(1, 12))]
         frames = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
-        check(frames, lead=rnd.randint(0, 300))
+        check(frames, lead=rnd.randint(0, 300), RL=rnd.choice([4, 8]))
     print("ok")

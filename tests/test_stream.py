@@ -23,7 +23,8 @@ def test_stream_algebra_matches_zlib():
         lens = [rnd.choice([0, 1, 2, 3, 4, 5, 7, 12, 15, 16, 17, 31, 60, 63, 64, 65, 100, 127, 128, 129, 250, 1500])
                 for _ in range(rnd.randint(1, 10))]
         frames = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
-        SA.check(frames, lead=rnd.randint(0, 300))
+        SA.check(frames, lead=rnd.randint(0, 300), RL=4)
+        SA.check(frames, lead=rnd.randint(0, 300), RL=8)
 
 
 def test_stream_algebra_operators():
@@ -60,36 +61,42 @@ def _run(cuda, var, data, off):
     return out.cpu().numpy().view(np.uint32)[:n]
 
 
-def _check(cuda, off, seed, name):
+VARS = [150, 153]  # streaming rows of 8 lanes (128-byte row steps) and of 4 lanes (64-byte)
+
+
+def _check(cuda, off, seed, name, var):
     from lneto_amd import synth
     from oracle import oracle as O
     data = synth.bytes_np(int(off[-1]) + 8, seed=seed)
-    got = _run(cuda, 150, data, off)
+    got = _run(cuda, var, data, off)
     want = O.crc32_frames(data, off, threads=8)
     bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, f"{name}: wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]}) of {len(off) - 1}"
+    assert bad.size == 0, f"{name} (variant {var}): wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]}) of {len(off) - 1}"
 
 
 @pytest.mark.gpu
-def test_gpu_stream_zipf(cuda):
+@pytest.mark.parametrize("var", VARS)
+def test_gpu_stream_zipf(cuda, var):
     from lneto_amd import synth
     for n, seed in ((1 << 16, 11), (1 << 20, 12), (300_001, 13)):
-        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}")
+        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stream_all_lengths(cuda):
+@pytest.mark.parametrize("var", VARS)
+def test_gpu_stream_all_lengths(cuda, var):
     from lneto_amd import synth
     rng = np.random.default_rng(9)
     for lead in (0, 1, 2, 3, 5, 64, 127):
         lens = rng.permutation(np.arange(0, 701))
         off = (synth.offsets_from_lengths(lens) + lead).astype(np.uint64)
         off = np.concatenate([[0], off]).astype(np.uint64)
-        _check(cuda, off, 100 + lead, f"lengths lead {lead}")
+        _check(cuda, off, 100 + lead, f"lengths lead {lead}", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stream_tiny_and_empty(cuda):
+@pytest.mark.parametrize("var", VARS)
+def test_gpu_stream_tiny_and_empty(cuda, var):
     """Frames inside one lane piece (the same-piece slow path), empty frames,
     and 8+ frame ends in one line (the offset-block stall path)."""
     from lneto_amd import synth
@@ -98,14 +105,15 @@ def test_gpu_stream_tiny_and_empty(cuda):
         lens = rng.choice([0, 0, 1, 2, 3, 4, 5, 7, 9, 15, 16, 17, 33, 64, 200], size=20000 + 977 * trial)
         off = synth.offsets_from_lengths(lens) + trial * 37
         off = np.concatenate([[0], off]).astype(np.uint64)
-        _check(cuda, off, 200 + trial, f"tiny {trial}")
+        _check(cuda, off, 200 + trial, f"tiny {trial}", var)
     # mixed: long runs of 64-byte frames (two events per line), then Zipf
     lens = np.concatenate([np.full(50000, 64), synth.zipf_lengths(50000, seed=5), np.full(3000, 1)])
-    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed")
+    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stream_slice_ends(cuda):
+@pytest.mark.parametrize("var", VARS)
+def test_gpu_stream_slice_ends(cuda, var):
     """Small batches: rows with zero or one frame, slices ending at every offset mod 128."""
     from lneto_amd import synth
     for n in (1, 2, 7, 127, 128, 129, 1000):
@@ -113,4 +121,4 @@ def test_gpu_stream_slice_ends(cuda):
             lens = synth.zipf_lengths(n, seed=n + pad)
             off = (synth.offsets_from_lengths(lens) + pad).astype(np.uint64)
             off = np.concatenate([[0], off]).astype(np.uint64)
-            _check(cuda, off, n * 7 + pad, f"n {n} pad {pad}")
+            _check(cuda, off, n * 7 + pad, f"n {n} pad {pad}", var)
