@@ -90,6 +90,27 @@ std::vector<uint32_t> build_stream_image(int64_t sb) {
   return img;
 }
 
+// The LDS image of the lane streams (stream_lanes.hpp): U = Z_4, then the
+// Z_c byte tables (c = 1..3), the Z_{64-4k} nibble tables (k = 0..15) and
+// the constants Z_{64-j}(0xFFFFFFFF) (lds_layout.hpp kLZc, kLZd, kLK).
+std::vector<uint32_t> build_lanes_image() {
+  std::vector<uint32_t> img(kLdsDwords, 0);
+  for (uint32_t m = 0; m < 4; ++m)
+    for (uint32_t e = 0; e < 256; ++e) {
+      const uint32_t v = zshift_bytes(e << (8 * m), 4);
+      for (uint32_t c = 0; c < 32; ++c) img[u_addr(m, e, c) / 4] = v;
+    }
+  for (uint32_t c = 1; c < 4; ++c)
+    for (uint32_t m = 0; m < 4; ++m)
+      for (uint32_t e = 0; e < 256; ++e) img[kLZc / 4 + (c - 1) * 1024 + 256 * m + e] = zshift_bytes(e << (8 * m), c);
+  for (uint32_t k = 0; k < 16; ++k)
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v)
+        img[kLZd / 4 + 128 * k + 16 * i + v] = zshift_bytes(v << (4 * i), 64 - 4 * (int64_t)k);
+  for (uint32_t j = 0; j < 64; ++j) img[kLK / 4 + j] = zshift_bytes(0xFFFFFFFFu, 64 - (int64_t)j);
+  return img;
+}
+
 // Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
 // byte tables for k = 0..5 (search_kernel.hip).
 // Then the tables of crc32_search_seg_kernel (24-byte lane segments): the
@@ -167,13 +188,15 @@ std::vector<uint32_t> compact_image(const std::vector<uint32_t>& full) {
   return c;
 }
 
-// The compact images back to back: [RL = 16][RL = 4][RL = 32][stream][stream64] (lds_layout.hpp image_index).
+// The compact images back to back: [RL = 16][RL = 4][RL = 32][stream][stream64][lanes] (lds_layout.hpp image_index).
 const std::vector<uint32_t>& host_image() {
   static const std::vector<uint32_t> img = [] {
     std::vector<uint32_t> all;
-    for (uint32_t rl : {16u, 4u, 32u, 8u, 9u}) {  // 8, 9: the stream images (128- and 64-byte row steps)
-      const std::vector<uint32_t> im =
-          compact_image(rl == 8 ? build_stream_image(128) : rl == 9 ? build_stream_image(64) : build_lds_image(rl));
+    for (uint32_t rl : {16u, 4u, 32u, 8u, 9u, 10u}) {  // 8, 9: the stream images (128- and 64-byte row steps); 10: lanes
+      const std::vector<uint32_t> im = compact_image(rl == 8    ? build_stream_image(128)
+                                                     : rl == 9  ? build_stream_image(64)
+                                                     : rl == 10 ? build_lanes_image()
+                                                                : build_lds_image(rl));
       all.insert(all.end(), im.begin(), im.end());
     }
     return all;

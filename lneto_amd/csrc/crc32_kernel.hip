@@ -1517,6 +1517,7 @@ constexpr uint64_t kLineMean = 4096;
 // (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
 constexpr uint64_t kLeanMean = 1600;
 #include "stream_rows.hpp"
+#include "stream_lanes.hpp"
 
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
@@ -1572,7 +1573,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     static_assert(kCompactUDwords == kBlockThreads, "one U value per thread");
     // (4-lane rows of four words per lane fold 16 virtual lanes: the RL = 16 image)
     const uint32_t* img = reinterpret_cast<const uint32_t*>(images) +
-                          image_index(strm ? (STR == 2 ? 9 : 8) : line ? 32 : (narrow && NW4 == 4) ? 16 : rl) *
+                          image_index(strm ? (STR == 3 ? 10 : STR == 2 ? 9 : 8) : line ? 32 : (narrow && NW4 == 4) ? 16 : rl) *
                               kCompactDwords;
     const uint32_t t = threadIdx.x;
     const uint32_t uv = img[t];
@@ -1670,9 +1671,13 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
     if constexpr (STR != 0 && !SEG && MODE != CrcMode::kAppend) {
       if (strm) {
-        constexpr int RLS = STR == 2 ? 4 : 8;
-        L.p = lane & (RLS - 1u), L.row = lane / RLS;
-        stream_body<MODE, VAR, RLS>(lds, L, cx);
+        if constexpr (STR == 3) {
+          lanes_body<MODE, VAR>(lds, L, cx);
+        } else {
+          constexpr int RLS = STR == 2 ? 4 : 8;
+          L.p = lane & (RLS - 1u), L.row = lane / RLS;
+          stream_body<MODE, VAR, RLS>(lds, L, cx);
+        }
         if (tl && lane == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
         return;
       }
@@ -1819,6 +1824,10 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 153: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
       case 154: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
       case 155: LNX_LAUNCH(CrcMode::kCrc, 152, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
+      // lane streams (stream_lanes.hpp): full, loads only, loads + chain only
+      case 160: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
+      case 161: LNX_LAUNCH(CrcMode::kCrc, 161, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
+      case 162: LNX_LAUNCH(CrcMode::kCrc, 162, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

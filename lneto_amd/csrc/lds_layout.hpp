@@ -51,7 +51,7 @@ constexpr uint32_t kLdsDwords = kLdsBytes / 4;
 constexpr uint32_t kFBase = 131072;                // start of the F region
 constexpr uint32_t kTBase = 147456;                // start of the T region
 constexpr uint32_t kCtrBase = 159744;              // frame-chunk counter (one dword)
-constexpr int kImageCount = 5;  // images: [0] RL = 16, [1] RL = 4, [2] RL = 32, [3] stream, [4] stream64
+constexpr int kImageCount = 6;  // images: [0] RL = 16, [1] RL = 4, [2] RL = 32, [3] stream, [4] stream64, [5] lanes
 // the streaming rows' image (stream_rows.hpp): U = Z_4, F column n = Z_{-4n},
 // then the Z_116 / Z_c / Z_{128-4k} / Z_1 tables at these byte addresses
 constexpr uint32_t kSZ116 = 147456;  // Z_{SB-12} byte tables (Z_116 / Z_52): entry (m, e) at 1024m + 4e
@@ -59,6 +59,12 @@ constexpr uint32_t kSTc = 151552;    // Z_c, c = 0..3, nibble p of the row: dwor
 constexpr uint32_t kSG = 153600;     // Z_{128-4k}, k = 0..4, nibble p: dword ((k*8 + p)*16 + v)
 constexpr uint32_t kSK = 156160;     // Z_{128-j}(0xFFFFFFFF), j = 0..15
 constexpr uint32_t kST1 = 156224;    // Z_1 byte table (slow-path byte steps)
+// the lane streams' image (stream_lanes.hpp): U = Z_4, then Z_c byte tables
+// (c = 1..3: dword (c-1)*1024 + 256m + e), Z_{64-4k} nibble tables (k = 0..15:
+// dword 128k + 16i + v) and the constants Z_{64-j}(0xFFFFFFFF), j = 0..63
+constexpr uint32_t kLZc = 131072;
+constexpr uint32_t kLZd = kLZc + 12288;
+constexpr uint32_t kLK = kLZd + 8192;
 
 constexpr uint32_t u_addr(uint32_t m, uint32_t e, uint32_t c) {
   return ((m >> 1) << 16) | (e << 8) | ((m & 1) << 7) | (c << 2);
@@ -70,8 +76,10 @@ constexpr uint32_t t_addr(uint32_t c, uint32_t h, uint32_t t, uint32_t v) {  // 
   return kTBase + ((48u * h + 16u * (t - 1) + v) << 7) + (c << 2);
 }
 static_assert(t_addr(31, 1, 3, 15) < kCtrBase, "T region overlaps the counter");
-// (8 and 9: the streaming rows' images with 128- and 64-byte row steps)
-constexpr int image_index(int rl) { return rl == 16 ? 0 : rl == 4 ? 1 : rl == 8 ? 3 : rl == 9 ? 4 : 2; }
+// (8 and 9: the streaming rows' images with 128- and 64-byte row steps; 10: the lane streams')
+constexpr int image_index(int rl) {
+  return rl == 16 ? 0 : rl == 4 ? 1 : rl == 8 ? 3 : rl == 9 ? 4 : rl == 10 ? 5 : 2;
+}
 
 // Compact image in HBM (what a workgroup reads at start): the 1024 distinct U
 // values U_m[e] at dword 256m + e, then the [kFBase, kLdsBytes) tail of the

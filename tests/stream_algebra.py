@@ -160,6 +160,76 @@ def check(frames: list[bytes], lead: int = 0, RL: int = 8) -> None:
     assert got == want, (got, want)
 
 
+def lane_stream(data: bytes, events: list[int], SB: int = 64) -> list[int]:
+    """CRCs of the frames [events[i], events[i+1]) by the lane-stream schedule
+    (stream_lanes.hpp): ONE lane folds the run serially, SB bytes (the kernel:
+    64) per superstep at q (SB-aligned), with no cross-lane combination:
+
+        y0 = r ^ w0, y_i = Z4(y_{i-1}) ^ w_i (i < SB/4), r' = Z4(y_last)
+
+    An event x in [q, q + SB) (cb = x - q, k = cb >> 2, c = cb & 3) reads the
+    chain's uncorrected state there from e = y_k ^ (w_k & ~lomask(c)):
+    S = Z_c(e); a frame start at x makes r' ^= Z_{SB-4k}(e) ^ Z_{SB-cb}(~0)
+    (= Z_{SB-cb}(S ^ ~0): the stream's state at x becomes ~0).  Only the last
+    start of a superstep corrects r' (the reset makes the earlier ones moot); a
+    later event of the same superstep corrects its S by Z_{x - x'}(S' ^ ~0), S'
+    the previous event's uncorrected state."""
+    m = len(events) - 1
+    out = []
+    if m < 0:
+        return out
+
+    def word(pos: int) -> int:
+        b = data[pos:pos + 4]
+        b = b + bytes(4 - len(b)) if len(b) < 4 else b
+        return int.from_bytes(b, "little")
+
+    q = events[0] & ~63  # the lane's first superstep: 64-byte aligned
+    r = 0
+    k = 0
+    nw = SB // 4
+    while k <= m:
+        w = [word(q + 4 * i) for i in range(nw)]
+        y = [r ^ w[0]]
+        for i in range(1, nw):
+            y.append(Zt(4, y[i - 1]) ^ w[i])
+        rn = Zt(4, y[-1])
+        fix = 0
+        first = True
+        Sp = 0
+        xp = 0
+        while k <= m and events[k] < q + SB:
+            x = events[k]
+            cb = x - q
+            kk, c = cb >> 2, cb & 3
+            e = y[kk] ^ (w[kk] & ~lomask(c) & MASK)
+            S = Zt(c, e) if c else e
+            corr = Zt(SB - 4 * kk, e) ^ Z(SB - cb, MASK)
+            St = S if first else S ^ Z(x - xp, Sp ^ MASK)
+            if k >= 1:
+                out.append(St ^ MASK)
+            if k < m:
+                fix = corr
+            Sp, xp, first = S, x, False
+            k += 1
+        r = rn ^ fix
+        q += SB
+    return out
+
+
+def check_lanes(frames: list[bytes], lead: int = 0, SB: int = 64) -> None:
+    buf = bytes(range(256)) * ((lead + 255) // 256)
+    data = bytearray(buf[:lead])
+    ev = [lead]
+    for f in frames:
+        data += f
+        ev.append(len(data))
+    data += bytes(range(7)) * 40
+    got = lane_stream(bytes(data), ev, SB)
+    want = [zlib.crc32(f) for f in frames]
+    assert got == want, (got, want)
+
+
 if __name__ == "__main__":
     import random
 
@@ -169,4 +239,5 @@ if __name__ == "__main__":
                 for _ in range(rnd.randint(1, 12))]
         frames = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
         check(frames, lead=rnd.randint(0, 300), RL=rnd.choice([4, 8]))
+        check_lanes(frames, lead=rnd.randint(0, 300), SB=rnd.choice([16, 64]))
     print("ok")

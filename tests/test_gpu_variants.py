@@ -32,7 +32,7 @@ pytestmark = pytest.mark.gpu
 #   steps, the RL = 16 image): 4 / 4 (16-frame chunks) / 3 / 5 steps per item
 # 150 / 153: the product dispatch with streaming rows (stream_rows.hpp) of 8 / 4 lanes for the narrow rows' frames
 FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97, 43, 44,
-          120, 124, 125, 126, 130, 138, 139, 140, 150, 153]
+          120, 124, 125, 126, 130, 138, 139, 140, 150, 153, 160]
 
 L.lib.lnx__crc32_variant.restype = ctypes.c_int
 L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,

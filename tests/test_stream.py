@@ -1,10 +1,13 @@
-"""Streaming rows (lneto_amd/csrc/stream_rows.hpp).
+"""Streaming rows (lneto_amd/csrc/stream_rows.hpp) and lane
+streams (lneto_amd/csrc/stream_lanes.hpp, §3.8).
 
 CPU: the schedule's algebra, restated in tests/stream_algebra.py, equals
 zlib's CRC-32 (Go hash/crc32 IEEE, the arithmetic of ethernet/crc.go:19-21) on
 frames of every small length, empty frames and frames inside one 16-byte lane
-piece (its slow path).  GPU: the kernel (profiling variant 150: the product
-dispatch with streaming rows for the narrow rows' workgroups) is bit-exact
+piece (its slow path); the lane streams' algebra likewise, with several
+frames inside one superstep.  GPU: the kernel (profiling variants 150 / 153:
+the product dispatch with 8- / 4-lane streaming rows for the narrow rows'
+workgroups; 160: with lane streams) is bit-exact
 against the C oracle on the Zipf mix, every length 0..700, runs of tiny and
 empty frames, and workgroup slices ending at every line offset."""
 import ctypes
@@ -25,6 +28,26 @@ def test_stream_algebra_matches_zlib():
         frames = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
         SA.check(frames, lead=rnd.randint(0, 300), RL=4)
         SA.check(frames, lead=rnd.randint(0, 300), RL=8)
+
+
+def test_lane_stream_algebra_matches_zlib():
+    rnd = random.Random(8)
+    for _ in range(200):
+        lens = [rnd.choice([0, 1, 2, 3, 4, 5, 7, 12, 15, 16, 17, 31, 60, 63, 64, 65, 100, 127, 128, 129, 250, 1500])
+                for _ in range(rnd.randint(1, 10))]
+        frames = [bytes(rnd.getrandbits(8) for _ in range(n)) for n in lens]
+        SA.check_lanes(frames, lead=rnd.randint(0, 300), SB=64)
+        SA.check_lanes(frames, lead=rnd.randint(0, 300), SB=16)
+
+
+def test_lane_stream_operators():
+    # the reset identity: Z_{64-4k}(e) ^ Z_{64-cb}(~0) == Z_{64-cb}(Z_c(e) ^ ~0), cb = 4k + c
+    rnd = random.Random(4)
+    for _ in range(50):
+        e = rnd.getrandbits(32)
+        k, c = rnd.randrange(16), rnd.randrange(4)
+        cb = 4 * k + c
+        assert SA.Z(64 - 4 * k, e) ^ SA.Z(64 - cb, 0xFFFFFFFF) == SA.Z(64 - cb, SA.Z(c, e) ^ 0xFFFFFFFF)
 
 
 def test_stream_algebra_operators():
@@ -61,7 +84,7 @@ def _run(cuda, var, data, off):
     return out.cpu().numpy().view(np.uint32)[:n]
 
 
-VARS = [150, 153]  # streaming rows of 8 lanes (128-byte row steps) and of 4 lanes (64-byte)
+VARS = [150, 153, 160]  # streaming rows of 8 lanes (128-byte row steps), of 4 lanes (64-byte), lane streams
 
 
 def _check(cuda, off, seed, name, var):
