@@ -162,6 +162,71 @@ __device__ __forceinline__ void lanes_body(const char* lds, const Lanes& L, cons
     }
     return e;
   };
+  // ---- VAR 164: the reset as a select inside the fold.  A
+  // frame starting at byte c of dword k makes the chain value there
+  // y = (~w_k & hm) ^ K_c (hm = ~0 << 8c, K_c = Z_{-c}(the top c bytes of ~0)),
+  // so Z4(y) is the new frame's state after the dword; only the ending
+  // frame's Z_c(e) is a lookup, off the fold's critical path.
+  constexpr auto unz = [](uint32_t v, int n) constexpr {
+    for (int i = 0; i < n; ++i) {
+      const uint32_t b = v >> 31, t = b ? v ^ 0xEDB88320u : v;
+      v = (t << 1) | b;
+    }
+    return v;
+  };
+  constexpr uint32_t kK1 = unz(0xFF000000u, 8), kK2 = unz(0xFFFF0000u, 16), kK3 = unz(0xFFFFFF00u, 24);
+  auto zc_of = [&](uint32_t e, uint32_t c) -> uint32_t {  // Z_c(e), c = 1..3
+    const uint32_t bc = kLZc + 4096u * ((c - 1u) & 3u);
+    return __builtin_amdgcn_bitop3_b32(lds_rd(lds, bc + ((e & 0xFFu) << 2)),
+                                       lds_rd(lds, bc + 1024u + (__builtin_amdgcn_ubfe(e, 8, 8) << 2)),
+                                       lds_rd(lds, bc + 2048u + (__builtin_amdgcn_ubfe(e, 16, 8) << 2)), 0x96) ^
+           lds_rd(lds, bc + 3072u + ((e >> 24) << 2));
+  };
+  auto corr_of = [&](uint32_t e, uint32_t rp) -> uint32_t {  // Z_{64-4k}(e) ^ Z_{64-rp}(~0)
+    const uint32_t bd = kLZd + 512u * ((rp >> 2) & 15u);
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i) v[i] = lds_rd(lds, bd + 64u * i + (__builtin_amdgcn_ubfe(e, 4 * i, 4) << 2));
+    const uint32_t t0 = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
+    const uint32_t t1 = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
+    const uint32_t t2 = __builtin_amdgcn_bitop3_b32(v[6], v[7], lds_rd(lds, kLK + (rp << 2)), 0x96);
+    return __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+  };
+  // an event's bookkeeping (the lanes with ev): the ended frame's result, the
+  // next boundary
+  auto advance = [&](bool ev, uint32_t St) {
+    if (wave_any(ev && k >= 1u && hold)) {  // a second end in this superstep: an extra store
+      if (ev && k >= 1u && hold) store_held();
+    }
+    const bool end = ev && k >= 1u;
+    const uint32_t crc = ~St;
+    hv = end ? (MODE == CrcMode::kCrc ? crc : (x - xs >= 4u && crc == 0x2144DF1Cu ? 1u : 0u)) : hv;
+    hf = end ? fa + k - 1u : hf;
+    hold = hold || end;
+    xs = ev ? x : xs;
+    k = ev ? k + 1u : k;
+    const bool adv = ev && k <= m && k - kb >= 4u;
+    if (wave_any(adv && !hasB)) {  // slow path: the next block is not here yet: load it now
+      uint32_t nb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) nb[i] = ld_rel(fa + kb + 4u + i <= fz ? fa + kb + 4u + i : kOOB);
+      if (adv && !hasB) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) B[i] = nb[i];
+        hasB = true, reqd = false;
+      }
+    }
+    if (adv) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[i] = B[i];
+      kb += 4u, hasB = false;
+    }
+    if (ev) {  // (selects by ia written as a ternary chain under a branch: hipcc keeps A in registers)
+      const uint32_t ia = k - kb;
+      x = k > m ? 0xFFFFFFFFu : ia == 0 ? A[0] : ia == 1 ? A[1] : ia == 2 ? A[2] : A[3];
+    }
+  };
+
   // one boundary of the superstep (the lanes where it lies in [P, P + 64)):
   // ye / we are the chain value and word of the first boundary's dword
   auto pass = [&](bool later, uint32_t ye, uint32_t we, uint32_t r0, const u32x4* Xs, uint32_t& fix, uint32_t& Sp,
@@ -259,6 +324,52 @@ __device__ __forceinline__ void lanes_body(const char* lds, const Lanes& L, cons
       if constexpr (VAR == 161) {  // profiling: loads only
 #pragma unroll
         for (int i = 0; i < 4; ++i) r ^= Xs[i][0] ^ Xs[i][1] ^ Xs[i][2] ^ Xs[i][3];
+      } else if constexpr (VAR == 164) {
+        const uint32_t r0 = r, rp1 = x - P, kev = rp1 >> 2, c1 = rp1 & 3u;  // kev >= 16: no boundary here
+        const uint32_t hm1 = 0xFFFFFFFFu << (8u * c1);
+        const uint32_t Kc = c1 == 1u ? kK1 : c1 == 2u ? kK2 : c1 == 3u ? kK3 : 0u;
+        const bool rst = k < m;  // the boundary starts frame fa + k
+        uint32_t y = 0, ec = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 16u; ++d) {
+          const uint32_t wd = Xs[d >> 2][d & 3u];
+          const uint32_t yn = d == 0 ? r0 ^ wd : u_step_xor(lds, y, wd, bu0, bu1);
+          const bool at = kev == d;
+          ec = at ? __builtin_amdgcn_bitop3_b32(yn, wd, hm1, 0x78) : ec;  // yn ^ (wd & hm1)
+          y = at && rst ? __builtin_amdgcn_bitop3_b32(wd, hm1, Kc, 0xA6) : yn;  // (~wd & hm1) ^ Kc
+        }
+        r = u_step(lds, y, bu0, bu1);
+        if (wave_any(rp1 < 64u)) {
+          const bool ev = rp1 < 64u;
+          uint32_t S = ec;
+          if (ev && c1 != 0u) S = zc_of(ec, c1);
+          const bool st1 = ev && rst;
+          advance(ev, S);
+          if (wave_any(x - P < 64u)) {  // more boundaries in this superstep (frames < 64 B)
+            uint32_t cin = 0, Sp = S, xp = rp1;  // cin: the correction the fold applied (relative to P)
+            if (st1) cin = corr_of(ec, rp1);
+            while (wave_any(x - P < 64u)) {
+              const uint32_t rp = x - P;
+              const bool evj = rp < 64u;
+              if (evj) {
+                const uint32_t c = rp & 3u, hm = 0xFFFFFFFFu << (8u * c);
+                const uint32_t e = e_at(r0, Xs, rp >> 2, hm);
+                const uint32_t Sj = c != 0u ? zc_of(e, c) : e;
+                uint32_t z = ~Sp;
+                for (uint32_t i = 0; i < rp - xp; ++i) z = z1(z);
+                const uint32_t St = Sj ^ z;
+                if (k < m) {
+                  const uint32_t cj = corr_of(e, rp);
+                  r ^= cin ^ cj;
+                  cin = cj;
+                }
+                Sp = Sj, xp = rp;
+                S = St;
+              }
+              advance(evj, S);
+            }
+          }
+        }
       } else {
         // the fold of the 16 dwords, keeping the first boundary's dword
         const uint32_t r0 = r, kev = (x - P) >> 2;  // >= 16: no boundary here
