@@ -1829,6 +1829,7 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 161: LNX_LAUNCH(CrcMode::kCrc, 161, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
       case 162: LNX_LAUNCH(CrcMode::kCrc, 162, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
       case 164: LNX_LAUNCH(CrcMode::kCrc, 164, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;  // reset in the fold
+      case 165: LNX_LAUNCH(CrcMode::kCrc, 165, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;  // + offsets on even sets only
       case 26: LNX_LAUNCH(CrcMode::kCrc, 1, 4); break;  // 4-lane rows, loads only
       case 27: LNX_LAUNCH(CrcMode::kCrc, 2, 4); break;  // 4-lane rows, math only
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;

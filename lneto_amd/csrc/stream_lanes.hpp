@@ -111,12 +111,24 @@ __device__ __forceinline__ void lanes_body(const char* lds, const Lanes& L, cons
   // is read (and transposed) first, then refilled for the superstep D ahead.
   u32x4 w[D][4];
   u32x4 ob[D][2];
+  constexpr bool HALF = VAR == 165 && D == 2;  // offset requests on even sets only (4 fewer VMEM per 2 supersteps)
   auto issue = [&](int s, uint32_t Pn, bool req, uint32_t kreq) {
     const uint32_t vp = Pn <= Pend ? Pn : kOOB;  // this lane's run, D supersteps ahead
     const uint32_t a0 = dpp_mov<0x00>(vp) + 16u * qi, a1 = dpp_mov<0x55>(vp) + 16u * qi,
                    a2 = dpp_mov<0xAA>(vp) + 16u * qi, a3 = dpp_mov<0xFF>(vp) + 16u * qi;
     const uint32_t f0 = fa + kreq, f2 = fa + kreq + 2u;
     const uint32_t vo0 = req && f0 <= nfb ? f0 * 8u : kOOB, vo1 = req && f2 <= nfb ? f2 * 8u : kOOB;
+    if (HALF && (s & 1)) {  // VAR 165: offsets only on even sets
+      asm volatile(
+          "s_nop 4\n\t"
+          "buffer_load_dwordx4 %0, %4, %8, 0 offen" LNX_LD_POL "\n\t"
+          "buffer_load_dwordx4 %1, %5, %8, 0 offen" LNX_LD_POL "\n\t"
+          "buffer_load_dwordx4 %2, %6, %8, 0 offen" LNX_LD_POL "\n\t"
+          "buffer_load_dwordx4 %3, %7, %8, 0 offen" LNX_LD_POL
+          : "=&v"(w[s][0]), "=&v"(w[s][1]), "=&v"(w[s][2]), "=&v"(w[s][3])
+          : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "s"(data_rsrc));
+      return;
+    }
     asm volatile(
         "s_nop 4\n\t"
         "buffer_load_dwordx4 %0, %6, %12, 0 offen" LNX_LD_POL "\n\t"
@@ -304,8 +316,14 @@ __device__ __forceinline__ void lanes_body(const char* lds, const Lanes& L, cons
     for (int s = 0; s < D; ++s) {
       // set s holds superstep P; younger: the store of its superstep, then D - 1
       // supersteps of (six loads, one store)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(1 + 7 * (D - 1)));
-      asm volatile("" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(w[s][2]), "+v"(w[s][3]), "+v"(ob[s][0]), "+v"(ob[s][1]));
+      if (HALF && s == 0)
+        asm volatile("s_waitcnt vmcnt(6)");  // younger: its store, the odd set's 4 loads and store
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(1 + 7 * (D - 1)));
+      if (HALF && (s & 1))
+        asm volatile("" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(w[s][2]), "+v"(w[s][3]));
+      else
+        asm volatile("" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(w[s][2]), "+v"(w[s][3]), "+v"(ob[s][0]), "+v"(ob[s][1]));
       u32x4 Xs[4] = {w[s][0], w[s][1], w[s][2], w[s][3]};
       {
         const bool b0 = (qi & 1u) != 0u, b1 = (qi & 2u) != 0u;
@@ -314,17 +332,17 @@ __device__ __forceinline__ void lanes_body(const char* lds, const Lanes& L, cons
         quad_swap<0x4E>(Xs[0], Xs[2], b1);
         quad_swap<0x4E>(Xs[1], Xs[3], b1);
       }
-      if (reqd && reqs == (uint32_t)s) {  // the requested block arrived
+      if (!(HALF && (s & 1)) && reqd && reqs == (uint32_t)s) {  // the requested block arrived
         B[0] = rel(ob[s][0][0]), B[1] = rel(ob[s][0][2]), B[2] = rel(ob[s][1][0]), B[3] = rel(ob[s][1][2]);
         hasB = true, reqd = false;
       }
-      const bool req = !hasB && !reqd && kb + 4u <= m;
+      const bool req = !hasB && !reqd && kb + 4u <= m && !(HALF && (s & 1));
       issue(s, P + 64u * D, req, kb + 4u);
       if (req) reqd = true, reqs = (uint32_t)s;
       if constexpr (VAR == 161) {  // profiling: loads only
 #pragma unroll
         for (int i = 0; i < 4; ++i) r ^= Xs[i][0] ^ Xs[i][1] ^ Xs[i][2] ^ Xs[i][3];
-      } else if constexpr (VAR == 164) {
+      } else if constexpr (VAR == 164 || VAR == 165) {
         const uint32_t r0 = r, rp1 = x - P, kev = rp1 >> 2, c1 = rp1 & 3u;  // kev >= 16: no boundary here
         const uint32_t hm1 = 0xFFFFFFFFu << (8u * c1);
         const uint32_t Kc = c1 == 1u ? kK1 : c1 == 2u ? kK2 : c1 == 3u ? kK3 : 0u;

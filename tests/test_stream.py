@@ -84,7 +84,7 @@ def _run(cuda, var, data, off):
     return out.cpu().numpy().view(np.uint32)[:n]
 
 
-VARS = [150, 153, 160, 164]  # streaming rows of 8 lanes (128-byte row steps), of 4 lanes (64-byte), lane streams (164: reset in the fold)
+VARS = [150, 153, 160, 164, 165]  # streaming rows of 8 lanes (128-byte row steps), of 4 lanes (64-byte), lane streams (164: reset in the fold)
 
 
 def _check(cuda, off, seed, name, var):
