@@ -14,12 +14,14 @@ every frame as one segment, random pseudo-header seeds) | ingress
 (lnx_ingress_verify_batch: the frames get Ethernet/IPv4/UDP headers written in
 place, so every frame takes the full header-sum + UDP-sum path).
 
-N=1 runs BASELINE configs[1] (1 M x 1500 B).  For N>1 (launched by
-torch.distributed.run, one rank per GPU) every rank owns its own contiguous
-slice of configs[4] (128 M x 1500 B over 8 GPUs = 16 M frames per GPU); frames
-are partitioned by index with no data-path collective (weak scaling).  The
-barrier / MAX-over-ranks timing uses torch.distributed (RCCL) only for the
-clock, never for data.
+N=1 runs BASELINE configs[1] (1 M x 1500 B) and, beside `value`, a "slice16m"
+sub-measurement: the same kernel over 16 M x 1500 B, the per-GPU slice the
+N>1 runs use, so the driver's scaling series has an equal-work N=1 point.  For
+N>1 (launched by torch.distributed.run, one rank per GPU) every rank owns its
+own contiguous slice of configs[4] (128 M x 1500 B over 8 GPUs = 16 M frames
+per GPU); frames are partitioned by index with no data-path collective (weak
+scaling).  The barrier / MAX-over-ranks timing runs over a gloo process group
+(host-side clock only): the path needs no RCCL, so none is initialised.
 
 Rank 0 prints ONE JSON line.  Extra fields: "roofline" (dominant kernel,
 HIP-event timed on its launch stream), "cpu_baseline" (the C oracle on the
@@ -202,6 +204,31 @@ def rx_ring_bench(args, L, synth, torch, dev, world):
     print(json.dumps(out), flush=True)
 
 
+def slice16m_bench(L, synth, torch, dev, steps: int = 10, warmup: int = 3):
+    """configs[4]'s per-GPU slice (16 M x 1500 B, 24 GB) on this one GPU: the
+    per-rank work of every N>1 run, so value_N / (N * slice16m) compares equal
+    launch sizes.  Reported beside `value`, never as it."""
+    n, flen = (1 << 27) // 8, FRAME_BYTES
+    d = synth.bytes_torch(n * flen, dev, seed=synth.SEED)
+    o = torch.arange(n + 1, dtype=torch.int64, device=dev) * flen
+    c = torch.empty(n, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        L.crc32_batch(d, o, out=c, stream=s)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        L.crc32_batch(d, o, out=c, stream=s)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    del d, o, c
+    torch.cuda.empty_cache()
+    return {"value": round(n * flen / el / 2**30, 2), "unit": "GiB/s", "ms_per_step": round(el * 1e3, 4),
+            "frames": n, "frame_bytes": flen, "steps": steps,
+            "frac_hbm": round(n * flen / el / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "configs[4] per-GPU slice on one GPU: the equal-work N=1 point of the scaling series"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +247,7 @@ def main():
                     help="bracket every N-th timed step with HIP events (kernel duration for the roofline); "
                          "an event pair on every step adds a few microseconds of GPU idle per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-slice16m", action="store_true", help="skip the 16 M-frame equal-work sub-measurement")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--with-copies", action="store_true", help="also time pinned H2D+kernel+D2H")
     ap.add_argument("--verify", action="store_true", help="spot-check results against the oracle")
@@ -236,24 +264,36 @@ def main():
         if world == 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
     # LNETO_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box only): every rank
-    # uses cuda:0 and the timing collectives run over gloo instead of RCCL.
+    # uses cuda:0.  LNETO_BENCH_CPU_RANKS=1 (CPU test of the N>1 control flow,
+    # tests/test_multi_gloo.py): no GPU at all, the step is the host C path.
     share = os.environ.get("LNETO_BENCH_SHARE_GPU") == "1"
+    cpu_ranks = os.environ.get("LNETO_BENCH_CPU_RANKS") == "1"
     gpu = 0 if share else local_rank
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
+    if cpu_ranks:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
+        # The barrier and the 2-float max-over-ranks are host-side: gloo.  The
+        # path has no exchange step, so no RCCL communicator
+        # is created (an 8-rank RCCL init would be a failure point unrelated to it).
         import torch.distributed as dist
-        if share:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-    cdev = torch.device("cpu") if share else dev  # device of the timing tensors
+        dist.init_process_group("gloo")
+    cdev = torch.device("cpu")  # device of the timing tensors (gloo)
 
     if args.op == "rx_ring":
         return rx_ring_bench(args, L, synth, torch, dev, world)
 
     wname, n_rank, flen, desc = workload_spec(args.workload, world)
+    if cpu_ranks:
+        if args.op != "crc32":
+            raise SystemExit("LNETO_BENCH_CPU_RANKS runs --op crc32 only")
+        # the control flow of an N-rank run on host cores: a small batch, the
+        # library's host CRC per frame (no GPU, no oracle)
+        n_rank = int(os.environ.get("LNETO_BENCH_CPU_FRAMES", "512"))
+        desc += f" [CPU rehearsal: {n_rank} frames per rank, host lnx_crc32, no GPU]"
     # Frame index slice of this rank within the global batch (weak scaling:
     # the global batch grows with N, every rank owns n_rank frames).
     n_total = n_rank * world
@@ -268,7 +308,11 @@ def main():
     d_bytes = synth.bytes_torch(nbytes, dev, seed=synth.SEED + lo * 0x10001)
     d_off = torch.from_numpy(off_np.astype(np.int64)).to(dev)
     d_crc = torch.empty(n_local, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = None if cpu_ranks else torch.cuda.current_stream(dev)
+
+    def sync():
+        if not cpu_ranks:
+            torch.cuda.synchronize(dev)
     if args.op == "sum16":
         d_seg = d_off[:-1].contiguous()
         d_len = (d_off[1:] - d_off[:-1]).to(torch.int32)
@@ -317,10 +361,16 @@ def main():
             # header CRC and the UDP CRC in place, idempotently, every step
             d_seg = d_off[:-1].contiguous()
             d_len = (d_off[1:] - d_off[:-1]).to(torch.int32)
-    torch.cuda.synchronize(dev)
+    sync()
+    host_frames = None
+    if cpu_ranks:
+        hb = d_bytes.numpy().tobytes()
+        host_frames = [hb[int(off_np[i]):int(off_np[i + 1])] for i in range(n_local)]
 
     def step():
-        if args.op == "sum16":
+        if cpu_ranks:
+            d_crc.copy_(torch.tensor([L.crc32(f) for f in host_frames], dtype=torch.int64).to(torch.int32))
+        elif args.op == "sum16":
             L.sum16_batch(d_bytes, d_seg, d_len, d_seed, out=d_sum, stream=stream)
         elif args.op == "fcs_verify":
             L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
@@ -344,18 +394,27 @@ def main():
     while time.perf_counter() - t_pw < args.prewarm_s:
         for _ in range(10):
             step()
-        torch.cuda.synchronize(dev)
+        sync()
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
 
     ev_every = max(1, args.event_every)
     timed = list(range(0, args.steps, ev_every))
-    starts = [torch.cuda.Event(enable_timing=True) for _ in timed]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in timed]
+    if cpu_ranks:  # host clock around the bracketed steps (no HIP events without a GPU)
+        class _Ev:
+            def record(self, _s):
+                self.t = time.perf_counter()
+
+            def elapsed_time(self, e):
+                return (e.t - self.t) * 1e3
+        starts, ends = [_Ev() for _ in timed], [_Ev() for _ in timed]
+    else:
+        starts = [torch.cuda.Event(enable_timing=True) for _ in timed]
+        ends = [torch.cuda.Event(enable_timing=True) for _ in timed]
     t0 = time.perf_counter()
     for k in range(args.steps):
         if k % ev_every == 0:
@@ -364,10 +423,10 @@ def main():
             ends[k // ev_every].record(stream)
         else:
             step()
-    torch.cuda.synchronize(dev)
+    sync()
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
@@ -449,10 +508,11 @@ def main():
     # run's kernel time.  For kernels bound by dependent LDS / VALU chains
     # (CRC32Search) these, not HBM, say how far the kernel is from its ceiling.
     counters_file = os.path.join(ROOT, "profiles", f"counters_{tag}.json")
-    if os.path.exists(counters_file):
+    if os.path.exists(counters_file) and not cpu_ranks:
         with open(counters_file) as fh:
             cn = json.load(fh)
-        clk, cus = 2.4e9, 256
+        # the clock the profiled run held (GRBM_GUI_ACTIVE over its kernel time), else the nominal 2.4 GHz
+        clk, cus = float(cn.get("clock_ghz_est") or 2.4) * 1e9, 256
         sec = kern_ms * 1e-3
         valu = cn["SQ_INSTS_VALU"] / sec
         comp = {"valu": {"achieved": round(valu / 1e9, 2), "peak": round(cus * 4 * 0.5 * clk / 1e9, 2),
@@ -465,9 +525,13 @@ def main():
                        "frac": round(busy / (cus * clk), 4), "instr_per_launch": cn["SQ_INSTS_LDS"],
                        "bank_conflict_cycles_per_launch": cn.get("SQ_LDS_BANK_CONFLICT")}
         comp["source"] = os.path.relpath(counters_file, ROOT)
+        comp["clock_ghz"] = round(clk / 1e9, 3)
+        # counts from another build of the kernel say nothing about this one:
+        # they are reported beside the HBM roofline, marked, and never replace it
+        comp["same_build"] = cn.get("lnx_version") == L.version()
         out["roofline_compute"] = comp
         top = max(("valu", "lds"), key=lambda k: comp[k]["frac"])
-        if comp[top]["frac"] > out["roofline"]["frac"]:
+        if comp["same_build"] and comp[top]["frac"] > out["roofline"]["frac"]:
             # the issue pipe, not HBM, is the nearer ceiling: it becomes the roofline, HBM moves beside it
             r = out["roofline"]
             r["hbm"] = {"achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"]}
@@ -514,6 +578,9 @@ def main():
                 want = O.crc32(fr)
             assert int(got[i]) == want, f"mismatch frame {i}"
         out["verified_sample"] = len(idx)
+
+    if world == 1 and args.op == "crc32" and wname == "mtu1500" and not cpu_ranks and not args.no_slice16m:
+        out["slice16m"] = slice16m_bench(L, synth, torch, dev)
 
     if args.with_copies and rank == 0:
         host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)

@@ -175,6 +175,41 @@ int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const 
 int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                              uint8_t* d_verdict, void* stream);
 
+/* The stack configuration behind the receive path's ErrPacketDrop checks, so
+ * that a frame the stack would not accept gets ErrPacketDrop (2) with the
+ * reference's precedence over the checksum verdicts:
+ *   StackEthernet.Demux (internet/stack-ethernet.go:146-161): before
+ *     ValidateSize, a frame that is neither broadcast nor for `mac` is dropped
+ *     unless eth_accept_multicast and the destination's group bit is set
+ *     (SetAcceptMulticast, :56-58); after it, an EtherType with no handler
+ *     (RegisterEthernet) is dropped;
+ *   demux4 (internet/stack-ip4.go:108-119,135-141): with ip4 != 0.0.0.0, a
+ *     destination other than ip4 is dropped before ValidateExceptCRC unless
+ *     ip4_accept_multicast and it is 224/4 or ip4_accept_broadcast and it is
+ *     255.255.255.255 (ipv4/definitions.go:17-36); a protocol with no handler
+ *     (bit p of ip4_protocols: byte p / 8, bit p % 8) is dropped after the
+ *     header sum and before the TCP / UDP sums;
+ *   demux6 (internet/stack-ip6.go:93-111): with ip6 != ::, a destination other
+ *     than ip6 is dropped before ValidateSize unless ip6_accept_multicast and
+ *     it is ff00::/8 (internal/ip.go:30-38); a next header with no handler is
+ *     dropped before the sums.
+ * A NULL filter is accept-all (lnx_ingress_verify_batch). */
+typedef struct lnx_rx_filter {
+  uint8_t mac[6];                 /* StackEthernetConfig.MAC */
+  uint8_t eth_accept_multicast;   /* StackEthernet.SetAcceptMulticast */
+  uint8_t ip4_accept_multicast;   /* stackip4 SetAcceptMulticast / SetAcceptBroadcast */
+  uint8_t ip4_accept_broadcast;
+  uint8_t ip6_accept_multicast;   /* stackip6 SetAcceptMulticast6 */
+  uint8_t ip4[4];                 /* stackip4 address, all zero = accept every destination */
+  uint8_t ip6[16];                /* stackip6 address, all zero = accept every destination */
+  uint16_t ethertypes[8];         /* EtherTypes with a registered handler */
+  uint32_t n_ethertypes;          /* entries of ethertypes in use (<= 8) */
+  uint8_t ip4_protocols[32];      /* 256-bit set of IP protocols with a handler on the IPv4 stack */
+  uint8_t ip6_protocols[32];      /* the same for the IPv6 stack */
+} lnx_rx_filter;
+int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                                      const lnx_rx_filter* filter, uint8_t* d_verdict, void* stream);
+
 /* Host-memory convenience: copies h_bytes/h_off to the device, runs
  * lnx_crc32_batch, copies the CRCs back, synchronously.  Used to measure the
  * PCIe-inclusive rate.  nbytes is the length of h_bytes; every
@@ -211,22 +246,35 @@ uint8_t* lnx_rx_ring_slots(lnx_rx_ring* ring);
 /* Pinned buffer length per slot (bytes of slot i in use, <= slot_cap). */
 uint32_t* lnx_rx_ring_lengths(lnx_rx_ring* ring);
 
+/* The ring's stack configuration for its verdicts (a copy of *filter is
+ * kept; NULL = accept-all, the default).  LNX_EINVAL for more than 8 EtherTypes. */
+int lnx_rx_ring_set_filter(lnx_rx_ring* ring, const lnx_rx_filter* filter);
+
+/* Device delivers frames without their FCS (x/netdev/interface.go:34-40 leaves
+ * the FCS to "device or stack"): no FCS check (fcs_ok = 1), verdicts on the
+ * whole frame. */
+#define LNX_RX_NO_FCS 4u
+
 /* netdev.Stack.IngressPackets (x/netdev/interface.go:82-89;
  * xnet.Netstack.IngressPackets, x/xnet/netstack.go:103-111) for slots
  * [first, first + count): the frame of slot i is slot[offset : len_i] and
- * carries its 4-byte LE FCS.  fcs_ok[k] = 1 iff that FCS is right (the check
- * lneto leaves to the PHY, x/netdev/interface.go:34-40); verdict[k] = the
- * receive path's checksum-stage verdict of the frame with the FCS stripped,
- * as lnx_ingress_verify_batch.  Host output arrays of `count` entries (either
- * may be NULL).  Synchronous; internally the slot range is pipelined over the
- * ring's stages (H2D, kernels, D2H on one HIP stream per stage). */
+ * carries its 4-byte LE FCS (unless LNX_RX_NO_FCS).  fcs_ok[k] = 1 iff that
+ * FCS is right (the check lneto leaves to the PHY, x/netdev/interface.go:34-40);
+ * verdict[k] = the receive path's checksum-stage verdict of the frame with the
+ * FCS stripped, as lnx_ingress_verify_batch_filtered with the ring's filter.
+ * Host output arrays of `count` entries (either may be NULL).  Synchronous;
+ * internally the slot range is pipelined over the ring's stages (H2D, kernels,
+ * D2H on one HIP stream per stage).  A batch whose frames fill less than 90 %
+ * of its slots is packed back to back on the host first, so the copy moves the
+ * frame bytes and their offsets, not whole slots. */
 int lnx_rx_ring_ingress(lnx_rx_ring* ring, uint32_t first, uint32_t count, uint32_t offset, uint32_t flags,
                         uint8_t* fcs_ok, uint8_t* verdict);
 
 /* The same for caller-owned buffers, exactly IngressPackets(bufs, offset):
- * frame k = bufs[k][offset : lens[k]] (lens[k] <= slot_cap).  The buffers are
- * gathered into the ring's slots (parallel host copies, overlapped with the
- * device work of the previous batch); nothing is retained after the call. */
+ * frame k = bufs[k][offset : lens[k]] (lens[k] <= slot_cap).  The frames are
+ * gathered back to back into pinned staging (parallel host copies, overlapped
+ * with the device work of the previous batch), so PCIe carries the frame bytes
+ * plus 8 bytes of offset per frame; nothing is retained after the call. */
 int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
                         uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict);
 
@@ -241,7 +289,9 @@ int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uin
  * length; status[k] (may be NULL) = the checksum step's status if non-zero,
  * else the append's (0, or 6 ErrShortBuffer with the frame unpadded).
  * Synchronous; the batches are pipelined over the ring's stages (gather, H2D,
- * kernels, D2H, scatter), nothing is retained after the call. */
+ * kernels, D2H, scatter), nothing is retained after the call.  Frames travel
+ * packed back to back, each with room for its padding and FCS only.  On an
+ * error return, lens and status are left as they were and no buffer is written. */
 #define LNX_TX_CHECKSUM 1u
 #define LNX_TX_FCS 2u
 int lnx_egress_packets(lnx_rx_ring* ring, uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset,

@@ -22,7 +22,7 @@ __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
     "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "LIB_PATH",
-    "CRC32_RESIDUE", "RxRing",
+    "CRC32_RESIDUE", "RxRing", "research_lib",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -515,6 +515,22 @@ class RxRing:
 
     def __del__(self):
         self.close()
+
+
+RESEARCH_LIB_PATH = os.path.join(HERE, "liblneto_amd_research.so")
+_research = None
+
+
+def research_lib():
+    """The research library (liblneto_amd_research.so): the same C-ABI plus the
+    losing kernel variants and the lnx__* profiling hooks of DESIGN.md §3-4.
+    Only tools/ and the variant tests use it; the product path never does."""
+    global _research
+    if _research is None:
+        if not os.path.exists(RESEARCH_LIB_PATH):
+            raise ImportError(f"{RESEARCH_LIB_PATH} is not built (make -C lneto_amd/csrc)")
+        _research = ctypes.CDLL(RESEARCH_LIB_PATH)
+    return _research
 
 
 def device_count() -> int:

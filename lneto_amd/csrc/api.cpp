@@ -16,9 +16,13 @@
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                bool verify, const void* image, int num_cus, hipStream_t stream);
+#ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
+hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
+                              uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
+#endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
                                  uint32_t trim);
@@ -28,8 +32,6 @@ hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, co
                                  void* out, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
-hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
-                              uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
@@ -60,6 +62,7 @@ std::vector<uint32_t> build_lds_image(uint32_t rl) {
   return img;
 }
 
+#ifdef LNX_RESEARCH
 // The LDS image of the streaming rows (stream_rows.hpp) with row steps of SB
 // bytes (128: 8-lane rows, 64: 4-lane rows): U = Z_4 (the chain's dword step),
 // F column n = Z_{-4n} (n = 0..31), then the Z_{SB-12} byte tables (the skip
@@ -110,6 +113,7 @@ std::vector<uint32_t> build_lanes_image() {
   for (uint32_t j = 0; j < 64; ++j) img[kLK / 4 + j] = zshift_bytes(0xFFFFFFFFu, 64 - (int64_t)j);
   return img;
 }
+#endif  // LNX_RESEARCH
 
 // Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
 // byte tables for k = 0..5 (search_kernel.hip).
@@ -163,6 +167,7 @@ struct DeviceCtx {
   void* d_image = nullptr;
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
+#ifdef LNX_RESEARCH
   // Per-stream scratch of the two-launch TX append (the CRCs between its
   // launches): calls on one stream run in order, so each stream reuses its
   // buffer; it grows, after a sync of that stream, when a batch outgrows it.
@@ -173,6 +178,7 @@ struct DeviceCtx {
   };
   std::mutex scratch_mu;
   std::vector<Scratch> scratch;
+#endif
 };
 
 constexpr int kMaxDevices = 64;
@@ -192,6 +198,7 @@ std::vector<uint32_t> compact_image(const std::vector<uint32_t>& full) {
 const std::vector<uint32_t>& host_image() {
   static const std::vector<uint32_t> img = [] {
     std::vector<uint32_t> all;
+#ifdef LNX_RESEARCH
     for (uint32_t rl : {16u, 4u, 32u, 8u, 9u, 10u}) {  // 8, 9: the stream images (128- and 64-byte row steps); 10: lanes
       const std::vector<uint32_t> im = compact_image(rl == 8    ? build_stream_image(128)
                                                      : rl == 9  ? build_stream_image(64)
@@ -199,6 +206,12 @@ const std::vector<uint32_t>& host_image() {
                                                                 : build_lds_image(rl));
       all.insert(all.end(), im.begin(), im.end());
     }
+#else
+    for (uint32_t rl : {16u, 4u, 32u}) {  // the product's row widths (image_index 0..2)
+      const std::vector<uint32_t> im = compact_image(build_lds_image(rl));
+      all.insert(all.end(), im.begin(), im.end());
+    }
+#endif
     return all;
   }();
   return img;
@@ -303,9 +316,12 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
   return LNX_OK;
 }
 
-// The calling device's scratch for `stream`, at least `bytes` long.
+#ifdef LNX_RESEARCH
+// The calling device's scratch for `stream`, at least `bytes` long.  The
+// caller holds c->scratch_mu until its launches on the scratch are enqueued,
+// so a concurrent grow (which syncs the stream, then frees) cannot free it
+// under a launch that is not yet in the stream.
 static int stream_scratch(DeviceCtx* c, hipStream_t stream, size_t bytes, void** out) {
-  std::lock_guard<std::mutex> lk(c->scratch_mu);
   DeviceCtx::Scratch* sc = nullptr;
   for (auto& x : c->scratch)
     if (x.stream == stream) sc = &x;
@@ -327,6 +343,7 @@ static int stream_scratch(DeviceCtx* c, hipStream_t stream, size_t bytes, void**
   *out = sc->p;
   return LNX_OK;
 }
+#endif  // LNX_RESEARCH
 
 int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                        uint32_t* d_crc, void* stream) {
@@ -357,10 +374,12 @@ int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_
   return LNX_OK;
 }
 
+#ifdef LNX_RESEARCH
 // TX append in two launches (A/B, lnx__fcs_append_variant 200): the segment-mode
 // CRC kernel into a compact per-stream scratch, then fcs_scatter_kernel.
 static int fcs_append_two_launch(DeviceCtx* c, uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n,
                                  uint32_t capacity, uint8_t* d_status, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(c->scratch_mu);  // held until both launches are enqueued
   uint32_t* scr = nullptr;
   int st = stream_scratch(c, s, n * sizeof(uint32_t), reinterpret_cast<void**>(&scr));
   if (st != LNX_OK) return st;
@@ -370,6 +389,7 @@ static int fcs_append_two_launch(DeviceCtx* c, uint8_t* d_bytes, const uint64_t*
   if (e != hipSuccess) return hip_fail(e, "fcs_scatter_kernel launch");
   return LNX_OK;
 }
+#endif  // LNX_RESEARCH
 
 int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                           uint8_t* d_status, void* stream) {
@@ -468,7 +488,9 @@ int lnx_crc32_batch_multi(int ngpu, const int* devices, const uint8_t* const* d_
   return LNX_OK;
 }
 
-// Profiling hook (not in include/lneto_amd.h): kernel variants of DESIGN.md §4.
+#ifdef LNX_RESEARCH
+// Profiling hooks of the research library (liblneto_amd_research.so, not in
+// include/lneto_amd.h): kernel variants of DESIGN.md §4.
 int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
                        void* stream) {
   if (n == 0) return LNX_OK;
@@ -531,6 +553,7 @@ int64_t lnx__crc32_timeline(int var, const uint8_t* d_bytes, const uint64_t* d_o
   if (e != hipSuccess) return hip_fail(e, "crc32 timeline launch");
   return LNX_OK;
 }
+#endif  // LNX_RESEARCH
 
 int lnx_device_count(void) {
   int n = 0;

@@ -1516,8 +1516,10 @@ constexpr uint64_t kLineMean = 4096;
 // Lean line rows (lines_body) from kShortMean up to this mean frame length
 // (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
 constexpr uint64_t kLeanMean = 1600;
+#ifdef LNX_RESEARCH  // the losing short-frame designs: research library only
 #include "stream_rows.hpp"
 #include "stream_lanes.hpp"
+#endif
 
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
           int CHW = 4, int CH4 = 32, bool SEG = false, int MIDW = 4, int KSM = 24, int SM = 1, int CHM = 4,
@@ -1669,6 +1671,7 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
     // chunks of the own slice from the LDS counter
     const WaveCtx cx = ctx_of(own);
     asm volatile("s_nop 4" ::: "memory");  // descriptors may be SGPRs just written by VALU readfirstlane
+#ifdef LNX_RESEARCH
     if constexpr (STR != 0 && !SEG && MODE != CrcMode::kAppend) {
       if (strm) {
         if constexpr (STR == 3) {
@@ -1682,6 +1685,9 @@ crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict_
         return;
       }
     }
+#else
+    static_assert(STR == 0 && VAR == 0, "variants are built into the research library only");
+#endif
     if (narrow) {
       L.p = lane & 3u, L.row = lane >> 2;
       rows_body<MODE, 4, KS4, S4, CH4, VAR, SEG, NW4, true, NSR4>(lds, L, cx);
@@ -1720,10 +1726,12 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
     // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
     if (verify)
       LNX_LAUNCH(CrcMode::kVerify, 0, 0, 24, 1, 12, 2, 4, 16, true);
+#ifdef LNX_RESEARCH
     else if (mode == CrcMode::kAppend && var == 4)  // profiling: FCS stored at once, no hold
       LNX_LAUNCH(CrcMode::kAppend, 4, 0, 24, 1, 12, 2, 4, 16, true);
     else if (mode == CrcMode::kAppend && var == 7)  // profiling: the FCS written with its 64-byte sector
       LNX_LAUNCH(CrcMode::kAppend, 7, 0, 24, 1, 12, 2, 4, 16, true);
+#endif
     else if (mode == CrcMode::kAppend)
       LNX_LAUNCH(CrcMode::kAppend, 0, 0, 24, 1, 12, 2, 4, 16, true);
     else
@@ -1731,6 +1739,10 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
   } else if (verify) {
     LNX_LAUNCH(CrcMode::kVerify, 0);
   } else {
+#ifndef LNX_RESEARCH
+    (void)var;
+    LNX_LAUNCH(CrcMode::kCrc, 0);
+#else
     // profiling variants (tools/prof/variants.py).  Arguments:
     // VAR, forced row width (0 = per workgroup), KSW, SW, KS4, S4, CHW, CH4,
     // SEG, MIDW, KSM, SM, CHM
@@ -1835,6 +1847,7 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       default: LNX_LAUNCH(CrcMode::kCrc, 0); break;
     }
 #undef LNX_16
+#endif  // LNX_RESEARCH
   }
 #undef LNX_LAUNCH
   return hipGetLastError();
@@ -1845,6 +1858,7 @@ hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64
                                const void* images, int num_cus, hipStream_t stream) {
   return launch_rows(0, verify ? CrcMode::kVerify : CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream);
 }
+#ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* images, int num_cus, hipStream_t stream, uint64_t* timeline) {
   // 80 / 81: the product with 2 / 4 workgroups per CU over the launch (one is
@@ -1853,6 +1867,7 @@ hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* o
     return launch_rows(0, CrcMode::kCrc, bytes, off, n, out, images, num_cus * (var == 80 ? 2 : 4), stream, nullptr);
   return launch_rows(var, CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream, timeline);
 }
+#endif
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                  void* out, const void* images, int num_cus, hipStream_t stream) {
   return launch_rows(0, CrcMode::kCrc, bytes, start, n, out, images, num_cus, stream, nullptr, len);
@@ -1866,7 +1881,8 @@ hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* le
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var) {
   return launch_rows(var, CrcMode::kAppend, bytes, start, n, status, images, num_cus, stream, nullptr, len, capacity);
 }
-// TX FCS append, second launch (lnx_fcs_append_batch): frame i's CRC, taken
+#ifdef LNX_RESEARCH
+// TX FCS append, second launch (lnx__fcs_append_variant 200): frame i's CRC, taken
 // by the segment-mode CRC kernel into a compact array, goes into the frame's
 // slot here, with the runt padding, the new length and the status
 // (internet/stack-ethernet.go:200-214; oracle.fcs_append).  Stores in place
@@ -1911,6 +1927,7 @@ hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* l
                      capacity, status);
   return hipGetLastError();
 }
+#endif  // LNX_RESEARCH
 
 // Waves of a launch (sizes the timeline buffer: 3 uint64 per wave).
 uint64_t crc32_launch_waves(uint64_t n, int num_cus) {

@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include "rx_filter.hpp"
 
 namespace lnx {
 
@@ -41,12 +42,21 @@ constexpr int kIngBlock = 256;
 // dwords per lane in flight: 24 (1536 B per row) reads a 1500-B frame in one
 // batch; 0.283 ms against 0.291 for 8 and 0.313 for 16 on 1 M x 1500 B
 // (bench.py --op ingress, LNX_PROF_INGRESS_UNROLL; profiles/r1g_ingress_unroll.txt)
-constexpr int kIngUnroll = 24;
+[[maybe_unused]] constexpr int kIngUnroll = 24;
 // qword lanes (r1h product): 12 qwords per lane in flight, again 1536 B per row
 constexpr int kIngUnrollQ = 12;
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
 constexpr uint32_t kVerifyEvilBit = 1, kVerifyIcmp = 2;
+
+// bit `proto` of a 256-bit mask held in kernel-argument words (a select chain:
+// no indexed scratch)
+__device__ __forceinline__ bool proto_bit(const uint32_t (&m)[8], uint32_t proto) {
+  const uint32_t w = proto >> 5;
+  const uint32_t word = w == 0 ? m[0] : w == 1 ? m[1] : w == 2 ? m[2] : w == 3 ? m[3] : w == 4 ? m[4]
+                        : w == 5 ? m[5] : w == 6 ? m[6] : m[7];
+  return (word >> (proto & 31u)) & 1u;
+}
 
 __device__ __forceinline__ uint32_t ing_keep_from(int32_t lo) {
   lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
@@ -88,11 +98,11 @@ template <int UNR, bool QW, bool GEN = false>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
-                      uint32_t trim) {
+                      uint32_t trim, RxFilter filt) {
   static_assert(!GEN || QW, "generate runs on the qword rows");
-  // offsets mode (seg_len null): frame f = bytes[off[f] : off[f+1]]; segment
-  // mode (the receive ring): frame f = bytes[off[f] : off[f] + seg_len[f] - trim],
-  // i.e. the FCS (trim = 4) is stripped, empty if seg_len[f] < trim
+  // offsets mode (seg_len null): frame f = bytes[off[f] : off[f+1] - trim];
+  // segment mode (the receive ring): frame f = bytes[off[f] : off[f] + seg_len[f] - trim],
+  // i.e. the FCS (trim = 4) is stripped, empty if the buffer is shorter than trim
   const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
   const uint64_t nwaves = (uint64_t)gridDim.x * (kIngBlock / 64);
   for (uint64_t q = (uint64_t)blockIdx.x * (kIngBlock / 64) + (threadIdx.x >> 6); q * 4 < n; q += nwaves) {
@@ -100,7 +110,8 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const bool live = f < n;
     const uint64_t s = live ? off[f] : 0;
     const uint32_t sl = live && seg_len ? seg_len[f] : 0u;
-    const uint64_t e = !live ? 0 : (seg_len ? s + (sl > trim ? sl - trim : 0u) : off[f + 1]);
+    const uint64_t e1 = live && !seg_len ? off[f + 1] : 0;
+    const uint64_t e = !live ? 0 : (seg_len ? s + (sl > trim ? sl - trim : 0u) : (e1 > s + trim ? e1 - trim : s));
     const uint64_t len64 = e > s ? e - s : 0;
     const uint32_t L = len64 < 0x7FFFFFFFull ? (uint32_t)len64 : 0x7FFFFFFFu;
     const uint8_t* fr = bytes + s;
@@ -234,21 +245,53 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
         }
       }
     } else {
+      // bytes o .. o + 3 of the frame (o >= 12, o + 3 < L), little-endian packed
+      auto field32 = [&](uint32_t o) -> uint32_t {
+        const int32_t kk = (int32_t)((o + mis) >> 2) - kstart;
+        return __builtin_amdgcn_alignbyte(rowword(kk + 1), rowword(kk), (o + mis) & 3u);
+      };
       if (L < 14) {
         v = kErrTruncatedFrame;
       } else {
         const uint32_t et = be(H0, 0);
-        if (et <= 1500 && L < et) {
+        bool eth_drop = false, et_handler = true;
+        if (filt.on) {
+          // StackEthernet.Demux (internet/stack-ethernet.go:146-152), before
+          // ValidateSize: a frame neither broadcast nor for the stack's MAC is
+          // dropped unless multicast frames are accepted and the group bit is set
+          const uint32_t* w = base + (mis >> 2);
+          const uint32_t sm = mis & 3u, m0 = w[0], m1 = w[1], m2 = w[2];
+          const uint32_t D0 = __builtin_amdgcn_alignbyte(m1, m0, sm), D1 = __builtin_amdgcn_alignbyte(m2, m1, sm) & 0xFFFFu;
+          const bool bcast = D0 == 0xFFFFFFFFu && D1 == 0xFFFFu;
+          const bool mine = D0 == filt.mac_lo && D1 == filt.mac_hi;
+          eth_drop = !bcast && !mine && !(filt.eth_mc && (D0 & 1u));
+          // handlers.demuxByProto(etype) (stack-ethernet.go:158-161): no handler -> drop
+          et_handler = false;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) et_handler = et_handler || (i < (int)filt.n_et && filt.et[i] == et);
+        }
+        if (eth_drop) {
+          v = kErrPacketDrop;
+        } else if (et <= 1500 && L < et) {
           v = kErrInvalidLengthField;
         } else if (et == 0x8100 && L < 18) {
           v = kErrTruncatedFrame;
+        } else if (!et_handler) {
+          v = kErrPacketDrop;
         } else if (et == 0x0800) {
           const uint32_t M = L - 14;
           if (M < 20) {
             v = kErrTruncatedFrame;
           } else {
             const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
-            if (tl < 20) v = kErrInvalidLengthField;
+            if (filt.on && filt.ip4 != 0u) {
+              // demux4's destination check (internet/stack-ip4.go:108-119), before ValidateExceptCRC
+              const uint32_t dst = field32(30);
+              const bool mc = (dst & 0xF0u) == 0xE0u, bc = dst == 0xFFFFFFFFu;  // ipv4/definitions.go:17-36
+              if (dst != filt.ip4 && !(filt.ip4_mc && mc) && !(filt.ip4_bc && bc)) v = kErrPacketDrop;
+            }
+            if (v != 0) {
+            } else if (tl < 20) v = kErrInvalidLengthField;
             else if (tl > M) v = kErrTruncatedFrame;
             else if (ihl < 5 || ihl * 4 > tl) v = kErrInvalidLengthField;
             else if ((b0 >> 4) != 4) v = kErrInvalidField;
@@ -256,7 +299,9 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
             if (v == 0) {
               hdr_sum = true;
               const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
-              if (proto == 6) {
+              if (filt.on && !proto_bit(filt.p4, proto)) {
+                v_udp4 = kErrPacketDrop;  // nodeByProto nil (stack-ip4.go:135-141), after the header sum
+              } else if (proto == 6) {
                 l4_sum = true;
                 pa = 26, pb = 34, la = 14 + hl, lb = 14 + tl;
                 lseed = ((tl - hl) & 0xFFFFu) + 6u;
@@ -294,8 +339,17 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
             v = kErrTruncatedFrame;
           } else {
             const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
-            if (pl + 40 > M) {
+            if (filt.on && (filt.ip6[0] | filt.ip6[1] | filt.ip6[2] | filt.ip6[3]) != 0u) {
+              // demux6's destination check (internet/stack-ip6.go:93-98), before ValidateSize
+              const uint32_t d0 = field32(38), d1 = field32(42), d2 = field32(46), d3 = field32(50);
+              const bool mine = d0 == filt.ip6[0] && d1 == filt.ip6[1] && d2 == filt.ip6[2] && d3 == filt.ip6[3];
+              if (!mine && !(filt.ip6_mc && (d0 & 0xFFu) == 0xFFu)) v = kErrPacketDrop;  // internal/ip.go:30-35
+            }
+            if (v != 0) {
+            } else if (pl + 40 > M) {
               v = kErrInvalidLengthField;
+            } else if (filt.on && !proto_bit(filt.p6, proto)) {
+              v = kErrPacketDrop;  // nodeByProto nil (stack-ip6.go:107-111), before the sums
             } else if (proto == 6 || proto == 17 || (proto == 58 && (flags & kVerifyIcmp))) {
               // demux6 size-checks the UDP header only; TCP goes straight to the
               // sum (internet/stack-ip6.go:116-137), whatever pl is.  ICMPv6:
@@ -477,13 +531,18 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
 
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
-                                 uint32_t trim) {
+                                 uint32_t trim, const RxFilter* filter) {
+  RxFilter filt{};
+  if (filter) filt = *filter;
   if (n == 0) return hipSuccess;
   const uint64_t frames_per_block = (kIngBlock / 64) * 4;
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   // 128 workgroups per CU (2 passes of 16 frames each at 1 M frames): 0.2594 ms against
   // 0.272 for 32, 0.2645 for 256 (profiles/r1h_grid_sweep.txt).
-  // profiling: LNX_PROF_INGRESS_WG_PER_CU overrides it
+#ifdef LNX_RESEARCH
+  // research library: LNX_PROF_INGRESS_WG_PER_CU overrides it;
+  // LNX_PROF_INGRESS_UNROLL=8|16|24 selects the dword-lane form with that
+  // batch depth (24 = the r1g product)
   static const uint64_t wg_per_cu = [] {
     const char* e = getenv("LNX_PROF_INGRESS_WG_PER_CU");
     const int v = e ? atoi(e) : 0;
@@ -491,24 +550,26 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   }();
   const uint64_t cap = (uint64_t)num_cus * wg_per_cu;
   if (grid > cap) grid = cap;
-  // profiling: LNX_PROF_INGRESS_UNROLL=8|16|24 selects the dword-lane form
-  // with that batch depth (24 = the r1g product)
   static const int unr = [] {
     const char* e = getenv("LNX_PROF_INGRESS_UNROLL");
     return e ? atoi(e) : 0;
   }();
   if (unr == 8)
     hipLaunchKernelGGL((ingress_verify_kernel<8, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
-                       off, n, flags, verdict, seg_len, trim);
+                       off, n, flags, verdict, seg_len, trim, filt);
   else if (unr == 16)
     hipLaunchKernelGGL((ingress_verify_kernel<16, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
-                       off, n, flags, verdict, seg_len, trim);
+                       off, n, flags, verdict, seg_len, trim, filt);
   else if (unr == kIngUnroll)
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnroll, false>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream, bytes,
-                       off, n, flags, verdict, seg_len, trim);
+                       off, n, flags, verdict, seg_len, trim, filt);
   else
+#else
+  const uint64_t cap = (uint64_t)num_cus * 128;
+  if (grid > cap) grid = cap;
+#endif
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream,
-                       bytes, off, n, flags, verdict, seg_len, trim);
+                       bytes, off, n, flags, verdict, seg_len, trim, filt);
   return hipGetLastError();
 }
 
@@ -523,7 +584,7 @@ hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint3
   const uint64_t cap = (uint64_t)num_cus * 128;
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, true>), dim3((unsigned)grid), dim3(kIngBlock), 0,
-                     stream, bytes, start, n, 0u, status, len, 0u);
+                     stream, bytes, start, n, 0u, status, len, 0u, RxFilter{});
   return hipGetLastError();
 }
 

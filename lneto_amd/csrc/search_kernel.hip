@@ -26,8 +26,8 @@
 
 namespace lnx {
 
-constexpr int kSearchBlock = 256;
-constexpr uint32_t kSearchTabBytes = 1024 + 6 * 4096;  // byte-step table + 6 x 4 byte tables
+[[maybe_unused]] constexpr int kSearchBlock = 256;
+[[maybe_unused]] constexpr uint32_t kSearchTabBytes = 1024 + 6 * 4096;  // byte-step table + 6 x 4 byte tables
 constexpr uint32_t kResidueRegister = 0xDEBB20E3u;     // ~0x2144DF1C
 
 // Z_{4*2^k}(x) through the four byte tables of level k
@@ -36,6 +36,7 @@ __device__ __forceinline__ uint32_t zlevel(const uint32_t* lds, int k, uint32_t 
   return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
 }
 
+#ifdef LNX_RESEARCH  // the r1 word-lane kernel (LNX_PROF_SEARCH=w)
 __global__ void __launch_bounds__(kSearchBlock)
 crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                     const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
@@ -96,6 +97,7 @@ crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restric
     if (lane == 0) result[c] = found;
   }
 }
+#endif  // LNX_RESEARCH
 
 // ------------------------------------------------------------------ segment lanes (r1g)
 // One wave per capture, blocks of 64 x SEG bytes: lane j owns the SEG bytes
@@ -132,7 +134,8 @@ __device__ __forceinline__ uint32_t zseg_xor(const uint32_t* z, uint32_t x, uint
 // (fewer VALU, bank conflicts) and the rest byte by byte through the
 // conflict-free byte column (more VALU, no conflicts); 2 of 6 balances the two
 // (r1h: 0.798 ms against 0.834 for 6, 0.804 for 3, 0.811 for 1, 0.814 for 0)
-constexpr int kSearchZWords = 2;
+[[maybe_unused]] constexpr int kSearchZWords = 2;
+
 template <bool kBallot, int kZWords>
 __global__ void __launch_bounds__(kSegBlock) __attribute__((amdgpu_waves_per_eu(8)))  // <= 64 VGPRs: 2 blocks per CU
 crc32_search_seg_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
@@ -747,7 +750,18 @@ crc32_search_u_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  // profiling: LNX_PROF_SEARCH=word selects the word-lane kernel
+#ifndef LNX_RESEARCH
+  // product: word checks, every Z_4 step through the lane-private U layout, one
+  // block per CU, two captures per half-wave (r2s2f)
+  {
+    uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+    if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
+    hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off, min_off,
+                       n, tables, result);
+  }
+#else
+  // research library:
+  // LNX_PROF_SEARCH=word selects the word-lane kernel
   // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B, =6 pass A all by Z_4,
   // =s the 24-byte-segment kernel (one capture per wave, the r1h product);
   // LNX_PROF_SEARCH_ZWORDS=0|2|4|8|10 the two-capture kernel's pass A split
@@ -863,6 +877,7 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
       }
     }
   }
+#endif  // LNX_RESEARCH
   return hipGetLastError();
 }
 

@@ -47,6 +47,7 @@ __device__ __forceinline__ uint32_t row_add16(uint32_t v) {
 // One 16-lane row per segment: lane p reads aligned dwords p, p+16, ... of the
 // segment's aligned span, kSumUnroll at a time, masks the bytes outside the
 // segment and accumulates E and O with v_dot4_u32_u8.
+#ifdef LNX_RESEARCH  // the r1c half-line rows (var 1)
 __global__ void __launch_bounds__(kSumBlock)
 sum16_segments_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                       const uint32_t* __restrict__ len, const uint32_t* __restrict__ seed,
@@ -87,6 +88,7 @@ sum16_segments_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     if (live && p == 0) out[i] = fold_sum16(sd + 256u * E + O);
   }
 }
+#endif  // LNX_RESEARCH
 
 // Line rows (round 1, r1g): the same row-per-segment split, but lane p loads
 // 8 bytes (global_load_dwordx2 nt) at 8p + 128k of the segment's 128-byte
@@ -108,6 +110,7 @@ __device__ __forceinline__ uint64_t keep8(int32_t d) {  // bytes [d, 8) of a qwo
 // ask for it twice within one batch, and with nt the second request found the
 // line gone from L2 and fetched it from HBM again (the CRC kernel's lean rows
 // showed the same, crc32_kernel.hip lines_body EP).
+
 template <bool NT, int UNR = kLineUnroll, bool EDGE = true>
 __global__ void __launch_bounds__(kSumBlock)
 sum16_lines_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
@@ -169,7 +172,8 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
   uint64_t grid = (n + seg_per_block - 1) / seg_per_block;
   // 256 workgroups per CU (one pass of 16 segments each at 1 M segments): 0.237-0.240 ms
   // against 0.259 for 32, 0.248 for 128 (profiles/r1h_grid_sweep.txt).
-  // profiling: LNX_PROF_SUM16_WG_PER_CU overrides it
+#ifdef LNX_RESEARCH
+  // research library: LNX_PROF_SUM16_WG_PER_CU overrides it, var picks the A/B form
   static const uint64_t wg_per_cu = [] {
     const char* e = getenv("LNX_PROF_SUM16_WG_PER_CU");
     const int v = e ? atoi(e) : 0;
@@ -193,6 +197,11 @@ hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, cons
     hipLaunchKernelGGL((sum16_lines_kernel<true, kLineUnroll, false>), dim3((unsigned)grid), dim3(kSumBlock), 0,
                        stream, bytes, off, len, seed, n, out);
   else
+#else
+  (void)var;
+  const uint64_t cap = (uint64_t)num_cus * 256;
+  if (grid > cap) grid = cap;
+#endif
     hipLaunchKernelGGL(sum16_lines_kernel<true>, dim3((unsigned)grid), dim3(kSumBlock), 0, stream, bytes, off,
                        len, seed, n, out);
   return hipGetLastError();

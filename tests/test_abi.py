@@ -89,3 +89,46 @@ def test_rows_kernel_algebra_emulated_on_cpu(tmp_path):
 def test_cpp_host_api_on_gpu(cuda, tmp_path):
     """The same C++ program on the MI355X: the ring opens and verifies FCS."""
     test_cpp_host_api_compiles_and_runs(tmp_path)
+
+
+def _kernels(path):
+    """Kernel symbols (mangled) in the .so's gfx950 code objects."""
+    out = subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", path, "/dev/stdout"],
+                         capture_output=True, check=True).stdout
+    return sorted(set(m.decode() for m in re.findall(rb"(_ZN3lnx\w+)\.kd", out)))
+
+
+def test_product_library_holds_only_product_kernels():
+    """The product .so carries exactly the shipped kernel instances: every
+    crc32_rows_kernel with VAR = 0 and no streaming form (STR = 0), one instance
+    each of sum16 / search / ring, ingress verify + TX generate; the research
+    variants live in liblneto_amd_research.so only."""
+    ks = _kernels(L.LIB_PATH)
+    rows = [k for k in ks if "crc32_rows_kernel" in k]
+    assert len(rows) == 5, rows  # offsets crc / verify, segments crc / verify / append
+    for k in rows:
+        assert re.search(r"CrcModeE\dELi0E", k), k          # VAR = 0
+        assert re.search(r"ELi0EEEvPKh", k), k              # STR = 0
+    others = sorted(re.sub(r"^_ZN3lnx\d+(\w+?kernel).*$", r"\1", k) for k in ks if k not in rows)
+    assert others == ["crc32_search_u_kernel", "ingress_verify_kernel", "ingress_verify_kernel",
+                      "ring_segments_kernel", "sum16_lines_kernel"], others
+    research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
+    if os.path.exists(research):
+        rk = _kernels(research)
+        assert set(ks) <= set(rk) and len(rk) > len(ks) + 40
+
+
+def test_product_library_reads_no_environment():
+    """No getenv in the product library's code (the LNX_PROF_* knobs are research-only)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", L.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert not re.search(r"\bgetenv\b", out), "product library imports getenv"
+    assert not hasattr_sym(L.lib, "lnx__crc32_variant")
+
+
+def hasattr_sym(lib, name):
+    try:
+        getattr(lib, name)
+        return True
+    except AttributeError:
+        return False

@@ -307,8 +307,8 @@ def test_sum16_kernel_variants_agree(cuda):
     launches each."""
     import ctypes
     import torch
-    L.lib.lnx__sum16_variant.restype = ctypes.c_int
-    L.lib.lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + \
+    L.research_lib().lnx__sum16_variant.restype = ctypes.c_int
+    L.research_lib().lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + \
         [ctypes.c_void_p] * 2
     rng = np.random.default_rng(23)
     n = 8192
@@ -323,7 +323,7 @@ def test_sum16_kernel_variants_agree(cuda):
     sd = torch.from_numpy(seeds.view(np.int32)).to(cuda)
     for var in (0, 1, 2, 3, 4, 5) * 3:
         out = torch.empty(n, dtype=torch.int16, device=cuda)
-        assert L.lib.lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n,
+        assert L.research_lib().lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n,
                                         out.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
         torch.cuda.synchronize()
         bad = np.nonzero(out.cpu().numpy().view(np.uint16) != want)[0]

@@ -34,15 +34,15 @@ pytestmark = pytest.mark.gpu
 FORCED = [10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 21, 22, 23, 24, 25, 28, 29, 40, 41, 42, 50, 51, 52, 56, 57, 60, 63, 70, 90, 92, 93, 97, 43, 44,
           120, 124, 125, 126, 130, 138, 139, 140, 150, 153, 160]
 
-L.lib.lnx__crc32_variant.restype = ctypes.c_int
-L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+L.research_lib().lnx__crc32_variant.restype = ctypes.c_int
+L.research_lib().lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_void_p, ctypes.c_void_p]
 
 
 def _run(var, d, o, n):
     import torch
     out = torch.empty(n, dtype=torch.int32, device=d.device)
-    rc = L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
+    rc = L.research_lib().lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()

@@ -20,9 +20,12 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path):
+@pytest.mark.parametrize("build", ["product", "research"])
+def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path, build):
+    """Both libraries: the product's instances and the research variants the GPU tests still run."""
+    flags = ["-DLNX_RESEARCH"] if build == "research" else []
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-                    "-c", "--save-temps",
+                    "-c", "--save-temps", *flags,
                     "-o", str(tmp_path / "k.o"), SRC], cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
     text = open(tmp_path / asm).read()
@@ -36,13 +39,16 @@ def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path):
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 @pytest.mark.parametrize("src", ["crc32_kernel", "sum16_kernel", "ingress_kernel", "search_kernel", "rx_ring"])
-def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src):
+@pytest.mark.parametrize("build", ["product", "research"])
+def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
     """tools/prof/audit_loops.py over every product kernel: no innermost loop
     that retires lanes with s_andn2_b64 exec and issues multi-dword loads (the
     shape of round 1's wrong-sum sum16 form)."""
     path = os.path.join(ROOT, "lneto_amd", "csrc", src + ".hip")
+    flags = ["-DLNX_RESEARCH"] if build == "research" else []
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-mllvm",
-                    "-amdgpu-atomic-optimizer-strategy=None", "-c", "--save-temps", "-o", str(tmp_path / "k.o"), path],
+                    "-amdgpu-atomic-optimizer-strategy=None", "-c", "--save-temps", *flags, "-o", str(tmp_path / "k.o"),
+                    path],
                    cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_loops.py"), str(tmp_path / asm)],

@@ -73,3 +73,30 @@ def test_world2_partition_matches_single_process():
         assert p.exitcode == 0
     assert got == want
     assert tmax == 2.0
+
+
+def test_bench_world2_on_cpu_ranks():
+    """bench.py's N>1 control flow end to end on host cores: torch.distributed.run
+    with 2 ranks, the gloo barrier and max-over-ranks (no RCCL), rank 0's one
+    JSON line with the whole-job value.  LNETO_BENCH_CPU_RANKS swaps the device
+    step for the library's host CRC so it runs without a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LNETO_BENCH_CPU_RANKS="1", LNETO_BENCH_CPU_FRAMES="256")
+    env.pop("LNETO_AMD_LIB", None)
+    port = _free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--steps", "4", "--warmup", "1", "--prewarm-s", "0", "--event-every", "2"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["steps"] == 4 and js["scaling"] == "weak"
+    assert js["config"]["frames_per_gpu"] == 256 and js["config"]["bytes_per_gpu"] == 256 * 1500
+    # whole-job value: both ranks' bytes over the max-over-ranks time
+    assert abs(js["value"] - 2 * 256 * 1500 * 4 / (js["ms_per_step"] * 4e-3) / 2**30) < 0.02 * js["value"] + 1e-3
+    assert "nccl" not in r.stderr.lower()

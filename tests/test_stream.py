@@ -64,8 +64,8 @@ def test_stream_algebra_operators():
 
 def _lib():
     import lneto_amd as L
-    L.lib.lnx__crc32_variant.restype = ctypes.c_int
-    L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+    L.research_lib().lnx__crc32_variant.restype = ctypes.c_int
+    L.research_lib().lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_void_p]
     return L
 
@@ -77,7 +77,7 @@ def _run(cuda, var, data, off):
     d = torch.from_numpy(data).to(cuda)
     o = torch.from_numpy(off.astype(np.int64)).to(cuda)
     out = torch.empty(max(n, 1), dtype=torch.int32, device=cuda)
-    rc = L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
+    rc = L.research_lib().lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()

@@ -129,7 +129,7 @@ def test_gpu_fcs_append_ab_variants(cuda, var, cap, base):
     import ctypes
     import torch
     import lneto_amd as L
-    fn = L.lib.lnx__fcs_append_variant
+    fn = L.research_lib().lnx__fcs_append_variant
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                    ctypes.c_void_p, ctypes.c_void_p]

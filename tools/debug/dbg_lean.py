@@ -6,8 +6,8 @@ import numpy as np, torch
 import lneto_amd as L
 from lneto_amd import synth
 from oracle import oracle as O
-L.lib.lnx__crc32_variant.restype = ctypes.c_int
-L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+L.research_lib().lnx__crc32_variant.restype = ctypes.c_int
+L.research_lib().lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_void_p, ctypes.c_void_p]
 wl, var = sys.argv[1], int(sys.argv[2])
 dev = torch.device("cuda:0")
@@ -18,7 +18,7 @@ o = torch.from_numpy(off.astype(np.int64)).to(dev)
 ref = L.crc32_batch(d, o).cpu().numpy().view(np.uint32)
 for rep in range(3):
     out = torch.zeros(n, dtype=torch.int32, device=dev)
-    assert L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
+    assert L.research_lib().lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
                                     torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)

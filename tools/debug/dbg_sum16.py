@@ -7,8 +7,8 @@ import numpy as np, torch
 import lneto_amd as L
 from lneto_amd import synth
 from oracle import oracle as O
-L.lib.lnx__sum16_variant.restype = ctypes.c_int
-L.lib.lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 2
+L.research_lib().lnx__sum16_variant.restype = ctypes.c_int
+L.research_lib().lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 2
 cuda = torch.device("cuda:0")
 rng = np.random.default_rng(21)
 n = 5000
@@ -34,7 +34,7 @@ for trial in range(16):
     if mode == "touch":
         _ = int(d.sum())
     out = torch.full((n,), 0x5A5A, dtype=torch.int16, device=cuda)
-    rc = L.lib.lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n, out.data_ptr(),
+    rc = L.research_lib().lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n, out.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint16)
@@ -42,7 +42,7 @@ for trial in range(16):
     sentinel = int((got[bad] == 0x5A5A).sum())
     again = np.zeros(0)
     if bad.size:
-        rc = L.lib.lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n,
+        rc = L.research_lib().lnx__sum16_variant(var, d.data_ptr(), o.data_ptr(), ln.data_ptr(), sd.data_ptr(), n,
                                       out.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         again = np.nonzero(out.cpu().numpy().view(np.uint16) != want)[0]

@@ -17,8 +17,8 @@ import torch
 import lneto_amd as L
 from lneto_amd import synth
 
-L.lib.lnx__fcs_append_variant.restype = ctypes.c_int
-L.lib.lnx__fcs_append_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+L.research_lib().lnx__fcs_append_variant.restype = ctypes.c_int
+L.research_lib().lnx__fcs_append_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 vars_ = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0+4").replace(",", "+").replace("m", "-").split("+")]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 9
@@ -41,7 +41,7 @@ def launch(var):
                                         ctypes.c_void_p(ln.data_ptr()), ctypes.c_uint64(n),
                                         ctypes.c_void_p(crc.data_ptr()), ctypes.c_void_p(s.cuda_stream)) == 0
         return
-    assert L.lib.lnx__fcs_append_variant(var, d.data_ptr(), start.data_ptr(), ln.data_ptr(), n, cap, st.data_ptr(),
+    assert L.research_lib().lnx__fcs_append_variant(var, d.data_ptr(), start.data_ptr(), ln.data_ptr(), n, cap, st.data_ptr(),
                                          s.cuda_stream) == 0
 
 

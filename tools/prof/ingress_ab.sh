@@ -7,6 +7,8 @@
 set -e
 O=gpurun_out/ingress_ab_$1
 mkdir -p $O
+# LNX_PROF_* knobs are read by the research library only
+export LNETO_AMD_LIB=$PWD/lneto_amd/liblneto_amd_research.so
 timeout -k 10 300 python -u -m pytest tests/test_ingress.py tests/test_rx_ring.py tests/test_tx_checksum.py -m gpu -x -q \
   --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 tail -1 $O/tests.log

@@ -2,6 +2,8 @@
 set -e
 O=gpurun_out/search_ab
 mkdir -p $O
+# LNX_PROF_* knobs are read by the research library only
+export LNETO_AMD_LIB=$PWD/lneto_amd/liblneto_amd_research.so
 export TMPDIR=/tmp
 timeout -k 10 200 python -u -m pytest tests/test_search.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 for m in 3 2 1 0; do

@@ -7,8 +7,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import numpy as np, torch
 import lneto_amd as L
 from lneto_amd import synth
-L.lib.lnx__sum16_variant.restype = ctypes.c_int
-L.lib.lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 2
+L.research_lib().lnx__sum16_variant.restype = ctypes.c_int
+L.research_lib().lnx__sum16_variant.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_uint64] + [ctypes.c_void_p] * 2
 dev = torch.device("cuda:0")
 off = synth.workload_offsets("mtu1500")
 n = len(off) - 1
@@ -18,7 +18,7 @@ ln = torch.from_numpy(np.diff(off).astype(np.int32)).to(dev)
 out = torch.empty(n, dtype=torch.int16, device=dev)
 s = torch.cuda.current_stream()
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-launch = lambda v: L.lib.lnx__sum16_variant(v, d.data_ptr(), o.data_ptr(), ln.data_ptr(), None, n, out.data_ptr(), s.cuda_stream)
+launch = lambda v: L.research_lib().lnx__sum16_variant(v, d.data_ptr(), o.data_ptr(), ln.data_ptr(), None, n, out.data_ptr(), s.cuda_stream)
 t0 = time.perf_counter()
 while time.perf_counter() - t0 < 0.5:
     launch(0)

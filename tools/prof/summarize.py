@@ -48,7 +48,9 @@ def main():
         try:
             for line in open(os.path.join(src, "bench_trace.log")):
                 if line.startswith("{"):
-                    steps = int(json.loads(line).get("steps", steps))
+                    js = json.loads(line)
+                    steps = int(js.get("steps", steps))
+                    summary["lnx_version"] = js.get("config", {}).get("kernel")
         except (OSError, ValueError):
             pass
         if d:
@@ -79,14 +81,15 @@ def main():
                        "method": "rocprofv3 --pmc FETCH_SIZE, own pass; x factor measured on tools/prof/calib "
                                  "(dword-per-lane reads of 2 GiB) in the same profiling run"}, fh, indent=1)
     c = summary["counters"]
-    keys = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT")
-    if all(k in c for k in keys):  # read by bench.py (roofline_compute)
-        with open(os.path.join(dst, f"counters_{wl}.json"), "w") as fh:
-            json.dump({**{k: c[k] for k in keys}, "source": f"{tag}_{wl}_summary.json",
-                       "method": "rocprofv3 --pmc, one counter group per pass (tools/prof/profile.sh), per-launch "
-                                 "averages over the traced dispatches; SQ_* summed over all CUs"}, fh, indent=1)
     if "GRBM_GUI_ACTIVE" in c and summary["avg_ns"]:
         summary["clock_ghz_est"] = c["GRBM_GUI_ACTIVE"] / 8 / summary["avg_ns"]
+    keys = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT")
+    if all(k in c for k in keys):  # read by bench.py (roofline_compute): tied to the build that made them
+        with open(os.path.join(dst, f"counters_{wl}.json"), "w") as fh:
+            json.dump({**{k: c[k] for k in keys}, "lnx_version": summary.get("lnx_version"),
+                       "clock_ghz_est": summary.get("clock_ghz_est"), "source": f"{tag}_{wl}_summary.json",
+                       "method": "rocprofv3 --pmc, one counter group per pass (tools/prof/profile.sh), per-launch "
+                                 "averages over the traced dispatches; SQ_* summed over all CUs"}, fh, indent=1)
     with open(os.path.join(dst, f"{tag}_{wl}_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     print(json.dumps(summary, indent=1))

@@ -16,7 +16,7 @@ import torch
 import lneto_amd as L
 from lneto_amd import synth
 
-f = L.lib.lnx__crc32_timeline
+f = L.research_lib().lnx__crc32_timeline
 f.restype = ctypes.c_int64
 f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
               ctypes.c_void_p]

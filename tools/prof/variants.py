@@ -16,8 +16,8 @@ import torch
 import lneto_amd as L
 from lneto_amd import synth
 
-L.lib.lnx__crc32_variant.restype = ctypes.c_int
-L.lib.lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+L.research_lib().lnx__crc32_variant.restype = ctypes.c_int
+L.research_lib().lnx__crc32_variant.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_void_p, ctypes.c_void_p]
 wl = sys.argv[1] if len(sys.argv) > 1 else "mtu1500"
 dev = torch.device("cuda:0")
@@ -37,7 +37,7 @@ print(f"lib {L.LIB_PATH}")
 
 
 def launch(var):
-    assert L.lib.lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream) == 0
+    assert L.research_lib().lnx__crc32_variant(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), s.cuda_stream) == 0
 
 
 t0 = time.perf_counter()
