@@ -189,14 +189,50 @@ inline int GenerateChecksumsBatch(uint8_t* d_bytes, const uint64_t* d_start, con
   return lnx_tx_checksum_batch(d_bytes, d_start, d_len, n, d_status, stream);
 }
 
+// The stack configuration the receive path consults before and between its
+// checksum checks (lnx_rx_filter): the Ethernet stack's MAC and multicast
+// acceptance (internet/stack-ethernet.go:56-58,146-152), the EtherTypes with a
+// handler (RegisterEthernet, :158-161), the IPv4 / IPv6 stacks' addresses,
+// multicast / broadcast acceptance and protocol handlers
+// (internet/stack-ip4.go:88-93,108-141, internet/stack-ip6.go:74,93-111).
+struct StackFilter {
+  uint8_t MAC[6] = {};
+  bool AcceptMulticastEthernet = false, AcceptMulticast4 = false, AcceptBroadcast4 = false,
+       AcceptMulticast6 = false;
+  uint8_t Addr4[4] = {};   // 0.0.0.0: every destination accepted (stack-ip4.go:108)
+  uint8_t Addr6[16] = {};  // ::: every destination accepted
+  std::vector<uint16_t> EtherTypes{0x0800, 0x86DD, 0x0806};
+  std::vector<uint8_t> Protocols4{1, 6, 17}, Protocols6{6, 17, 58};
+
+  // The C-ABI form; false for more than 8 EtherTypes.
+  bool ToC(lnx_rx_filter* f) const {
+    if (EtherTypes.size() > 8) return false;
+    *f = lnx_rx_filter{};
+    for (int i = 0; i < 6; ++i) f->mac[i] = MAC[i];
+    f->eth_accept_multicast = AcceptMulticastEthernet, f->ip4_accept_multicast = AcceptMulticast4;
+    f->ip4_accept_broadcast = AcceptBroadcast4, f->ip6_accept_multicast = AcceptMulticast6;
+    for (int i = 0; i < 4; ++i) f->ip4[i] = Addr4[i];
+    for (int i = 0; i < 16; ++i) f->ip6[i] = Addr6[i];
+    f->n_ethertypes = uint32_t(EtherTypes.size());
+    for (size_t i = 0; i < EtherTypes.size(); ++i) f->ethertypes[i] = EtherTypes[i];
+    for (uint8_t p : Protocols4) f->ip4_protocols[p >> 3] |= uint8_t(1u << (p & 7));
+    for (uint8_t p : Protocols6) f->ip6_protocols[p >> 3] |= uint8_t(1u << (p & 7));
+    return true;
+  }
+};
+
 // Receive-path checksum verdicts of every Ethernet frame (0 or the lneto
 // errGeneric code), StackEthernet.Demux -> demux4 / demux6.
-// icmp: the ICMP clients' checks too (LNX_VERIFY_ICMP).
+// icmp: the ICMP clients' checks too (LNX_VERIFY_ICMP).  With a StackFilter,
+// frames the stack would not accept get ErrPacketDrop where lneto drops them.
 inline int VerifyIngressBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_verdict,
-                              bool evilBit = false, void* stream = nullptr, bool icmp = false) {
-  return lnx_ingress_verify_batch(d_frames, d_off, n,
-                                  (evilBit ? LNX_VERIFY_EVIL_BIT : 0u) | (icmp ? LNX_VERIFY_ICMP : 0u), d_verdict,
-                                  stream);
+                              bool evilBit = false, void* stream = nullptr, bool icmp = false,
+                              const StackFilter* filter = nullptr) {
+  const uint32_t flags = (evilBit ? LNX_VERIFY_EVIL_BIT : 0u) | (icmp ? LNX_VERIFY_ICMP : 0u);
+  if (!filter) return lnx_ingress_verify_batch(d_frames, d_off, n, flags, d_verdict, stream);
+  lnx_rx_filter f;
+  if (!filter->ToC(&f)) return LNX_EINVAL;
+  return lnx_ingress_verify_batch_filtered(d_frames, d_off, n, flags, &f, d_verdict, stream);
 }
 }  // namespace internet
 
@@ -221,15 +257,45 @@ class RxRing {
   // Slot i's pinned buffer (slotCap bytes) and its length, for a producer.
   uint8_t* Slot(uint32_t i) { return lnx_rx_ring_slots(r_) + size_t(i) * cap_; }
   uint32_t& Len(uint32_t i) { return lnx_rx_ring_lengths(r_)[i]; }
+  // The stack's destination and handler configuration for the verdicts
+  // (nullptr: accept-all), and whether the device strips the FCS
+  // (x/netdev/interface.go:34-40: then no FCS check, verdicts on whole frames).
+  int SetFilter(const internet::StackFilter* f) {
+    if (!f) return lnx_rx_ring_set_filter(r_, nullptr);
+    lnx_rx_filter c;
+    if (!f->ToC(&c)) return LNX_EINVAL;
+    return lnx_rx_ring_set_filter(r_, &c);
+  }
+  void SetDeviceStripsFCS(bool v) { noFCS_ = v; }
   // Slots [first, first + count) as IngressPackets(slots, offset).
   int Ingress(uint32_t first, uint32_t count, uint32_t offset, uint8_t* fcsOK, uint8_t* verdict,
               bool evilBit = false) {
-    return lnx_rx_ring_ingress(r_, first, count, offset, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, fcsOK, verdict);
+    return lnx_rx_ring_ingress(r_, first, count, offset, flags(evilBit), fcsOK, verdict);
   }
-  // Caller-owned buffers (gathered into the slots).
+  // Caller-owned buffers (gathered into pinned staging for the call only).
   int IngressPackets(const uint8_t* const* bufs, const uint32_t* lens, uint64_t n, uint32_t offset, uint8_t* fcsOK,
                      uint8_t* verdict, bool evilBit = false) {
-    return lnx_ingress_packets(r_, bufs, lens, n, offset, evilBit ? LNX_VERIFY_EVIL_BIT : 0u, fcsOK, verdict);
+    return lnx_ingress_packets(r_, bufs, lens, n, offset, flags(evilBit), fcsOK, verdict);
+  }
+  // IngressPackets(bufs [][]byte, offset int) with the Go slice shape: the
+  // buffers' addresses and lengths are staged in the ring object for the call
+  // only and dropped after it (the Go binding pins them with runtime.Pinner
+  // for exactly that span); fcsOK / verdict are resized.
+  int IngressPackets(const std::vector<lneto::Bytes>& bufs, uint32_t offset, std::vector<uint8_t>& fcsOK,
+                     std::vector<uint8_t>& verdict, bool evilBit = false) {
+    ptrs_.resize(bufs.size());
+    lens_.resize(bufs.size());
+    for (size_t k = 0; k < bufs.size(); ++k) {
+      ptrs_[k] = bufs[k].p;
+      lens_[k] = uint32_t(bufs[k].n);
+    }
+    fcsOK.resize(bufs.size());
+    verdict.resize(bufs.size());
+    const int rc = lnx_ingress_packets(r_, ptrs_.data(), lens_.data(), bufs.size(), offset, flags(evilBit),
+                                       fcsOK.data(), verdict.data());
+    ptrs_.clear();  // unpinned: nothing refers to the caller's buffers after the call
+    lens_.clear();
+    return rc;
   }
   // netdev.Stack.EgressPackets(bufs, sizes, offset) (x/netdev/interface.go:85)
   // for the device's part of the transmit path: frame k = bufs[k][offset :
@@ -244,7 +310,11 @@ class RxRing {
   uint32_t SlotCap() const { return cap_; }
 
  private:
+  uint32_t flags(bool evilBit) const { return (evilBit ? LNX_VERIFY_EVIL_BIT : 0u) | (noFCS_ ? LNX_RX_NO_FCS : 0u); }
   lnx_rx_ring* r_ = nullptr;
   uint32_t nslots_ = 0, cap_ = 0;
+  bool noFCS_ = false;
+  std::vector<const uint8_t*> ptrs_;
+  std::vector<uint32_t> lens_;
 };
 }  // namespace netdev

@@ -22,7 +22,7 @@ __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
     "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "LIB_PATH",
-    "CRC32_RESIDUE", "RxRing", "research_lib",
+    "CRC32_RESIDUE", "RxRing", "RxFilter", "RX_NO_FCS", "research_lib",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -57,6 +57,41 @@ lib = ctypes.CDLL(LIB_PATH)
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
+
+
+class RxFilter(ctypes.Structure):
+    """lnx_rx_filter (include/lneto_amd.h): the stack configuration behind the
+    receive verdicts' ErrPacketDrop checks (internet/stack-ethernet.go:146-161,
+    internet/stack-ip4.go:108-141, internet/stack-ip6.go:93-111).  Build it with
+    RxFilter.make(mac=..., ip4=..., ...)."""
+    _fields_ = [
+        ("mac", ctypes.c_uint8 * 6), ("eth_accept_multicast", ctypes.c_uint8),
+        ("ip4_accept_multicast", ctypes.c_uint8), ("ip4_accept_broadcast", ctypes.c_uint8),
+        ("ip6_accept_multicast", ctypes.c_uint8), ("ip4", ctypes.c_uint8 * 4), ("ip6", ctypes.c_uint8 * 16),
+        ("ethertypes", ctypes.c_uint16 * 8), ("n_ethertypes", ctypes.c_uint32),
+        ("ip4_protocols", ctypes.c_uint8 * 32), ("ip6_protocols", ctypes.c_uint8 * 32),
+    ]
+
+    @classmethod
+    def make(cls, mac: bytes, ethertypes=(0x0800, 0x86DD, 0x0806), ip4: bytes = bytes(4), ip6: bytes = bytes(16),
+             ip4_protocols=(1, 6, 17), ip6_protocols=(6, 17, 58), eth_accept_multicast: bool = False,
+             ip4_accept_multicast: bool = False, ip4_accept_broadcast: bool = False,
+             ip6_accept_multicast: bool = False) -> "RxFilter":
+        if len(mac) != 6 or len(ip4) != 4 or len(ip6) != 16 or len(ethertypes) > 8:
+            raise LnetoError("RxFilter: mac 6 bytes, ip4 4, ip6 16, at most 8 EtherTypes")
+        f = cls()
+        f.mac[:] = list(mac)
+        f.ip4[:] = list(ip4)
+        f.ip6[:] = list(ip6)
+        f.eth_accept_multicast, f.ip4_accept_multicast = int(eth_accept_multicast), int(ip4_accept_multicast)
+        f.ip4_accept_broadcast, f.ip6_accept_multicast = int(ip4_accept_broadcast), int(ip6_accept_multicast)
+        f.n_ethertypes = len(ethertypes)
+        for i, et in enumerate(ethertypes):
+            f.ethertypes[i] = et
+        for arr, protos in ((f.ip4_protocols, ip4_protocols), (f.ip6_protocols, ip6_protocols)):
+            for p in protos:
+                arr[p >> 3] |= 1 << (p & 7)
+        return f
 _sig = {
     "lnx_crc32_update": (ctypes.c_uint32, [ctypes.c_uint32, _u8p, ctypes.c_size_t]),
     "lnx_crc32": (ctypes.c_uint32, [_u8p, ctypes.c_size_t]),
@@ -69,6 +104,9 @@ _sig = {
     "lnx_fcs_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_sum16_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_ingress_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
+    "lnx_ingress_verify_batch_filtered": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                                         ctypes.POINTER(RxFilter), _vp, _vp]),
+    "lnx_rx_ring_set_filter": (ctypes.c_int, [_vp, ctypes.POINTER(RxFilter)]),
     "lnx_crc32_search_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_crc32_segments": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_fcs_append_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
@@ -353,21 +391,27 @@ def crc32_search_batch(d_bytes, d_off, d_min_off=None, out=None, stream=None):
 
 VERIFY_EVIL_BIT = 1  # LNX_VERIFY_EVIL_BIT
 VERIFY_ICMP = 2      # LNX_VERIFY_ICMP
+RX_NO_FCS = 4        # LNX_RX_NO_FCS: the device strips the FCS (x/netdev/interface.go:34-40)
 TX_CHECKSUM, TX_FCS = 1, 2  # LNX_TX_CHECKSUM, LNX_TX_FCS
 
 
-def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None):
-    """Receive-path checksum verdict per Ethernet frame (lnx_ingress_verify_batch):
-    0 = checks passed / none apply, else lneto's errGeneric code (3 = ErrBadCRC, ...)."""
+def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None, filter: RxFilter | None = None):
+    """Receive-path checksum verdict per Ethernet frame (lnx_ingress_verify_batch,
+    or lnx_ingress_verify_batch_filtered with a stack ``filter``): 0 = checks
+    passed / none apply, else lneto's errGeneric code (3 = ErrBadCRC, 2 = ErrPacketDrop, ...)."""
     import torch
-    what = "lnx_ingress_verify_batch"
+    what = "lnx_ingress_verify_batch" if filter is None else "lnx_ingress_verify_batch_filtered"
     b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
     out = _out(what, out, n, torch.uint8, "u8", b.device)
     if n > 0:
         with b as s:
-            _check(lib.lnx_ingress_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags, out.data_ptr(), s),
-                   what)
+            if filter is None:
+                rc = lib.lnx_ingress_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags, out.data_ptr(), s)
+            else:
+                rc = lib.lnx_ingress_verify_batch_filtered(d_bytes.data_ptr(), d_off.data_ptr(), n, flags,
+                                                           ctypes.byref(filter), out.data_ptr(), s)
+            _check(rc, what)
     return out
 
 
@@ -457,6 +501,11 @@ class RxRing:
             nslots, slot_cap)
         self.lengths = np.ctypeslib.as_array((ctypes.c_uint32 * nslots).from_address(lp))
 
+    def set_filter(self, filt: RxFilter | None) -> None:
+        """The ring's stack configuration (lnx_rx_ring_set_filter); None = accept-all."""
+        _check(lib.lnx_rx_ring_set_filter(self._h, ctypes.byref(filt) if filt is not None else None),
+               "lnx_rx_ring_set_filter")
+
     def ingress(self, first: int = 0, count: int | None = None, offset: int = 0, flags: int = 0):
         import numpy as np
         if count is None:
@@ -469,6 +518,8 @@ class RxRing:
 
     def ingress_packets(self, bufs, offset: int = 0, flags: int = 0):
         import numpy as np
+        if not isinstance(offset, int) or not 0 <= offset < 2**32:
+            raise LnetoError("ingress_packets: offset must be an int in [0, 2**32)")
         arrs = [np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray)
                 else np.ascontiguousarray(b, dtype=np.uint8) for b in bufs]
         n = len(arrs)
@@ -488,13 +539,20 @@ class RxRing:
         are finished in place; returns (new sizes, status) as uint32 / uint8 arrays."""
         import numpy as np
         n = len(bufs)
+        if not isinstance(offset, int) or not 0 <= offset < 2**32:
+            raise LnetoError("egress_packets: offset must be an int in [0, 2**32)")
+        if not isinstance(capacity, (int, type(None))) or (capacity is not None and not 0 <= capacity < 2**32):
+            raise LnetoError("egress_packets: capacity must be an int in [0, 2**32)")
         for b in bufs:
             if not isinstance(b, np.ndarray) or b.dtype != np.uint8 or not b.flags.c_contiguous \
                     or not b.flags.writeable:
                 raise LnetoError("egress_packets: bufs must be writable contiguous uint8 numpy arrays")
         if capacity is None:
             capacity = self.slot_cap
-        lens = np.ascontiguousarray(np.asarray(sizes, dtype=np.uint32)).copy()
+        sz = np.asarray(sizes)
+        if sz.size and (sz.dtype.kind not in "iu" or sz.min() < 0 or sz.max() >= 2**32):
+            raise LnetoError("egress_packets: sizes must be non-negative integers below 2**32")
+        lens = np.ascontiguousarray(sz.astype(np.uint32)).copy()
         if len(lens) != n:
             raise LnetoError("egress_packets: one size per buffer")
         for b, l in zip(bufs, lens):  # the finished frame is written back at bufs[k][offset:]

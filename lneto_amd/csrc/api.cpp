@@ -12,6 +12,7 @@
 #include "../../include/lneto_amd.h"
 #include "gf2.hpp"
 #include "lds_layout.hpp"
+#include "rx_filter.hpp"
 
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
@@ -25,7 +26,7 @@ hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* l
 #endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
-                                 uint32_t trim);
+                                 uint32_t trim, const RxFilter* filter);
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
@@ -418,13 +419,20 @@ int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const 
 
 int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                              uint8_t* d_verdict, void* stream) {
+  return lnx_ingress_verify_batch_filtered(d_bytes, d_off, n, flags, nullptr, d_verdict, stream);
+}
+
+int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                                      const lnx_rx_filter* filter, uint8_t* d_verdict, void* stream) {
+  RxFilter filt;
+  if (!rx_filter_of(filter, &filt)) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   if (!d_bytes || !d_off || !d_verdict) return LNX_EINVAL;
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags, d_verdict, c->num_cus,
-                                       static_cast<hipStream_t>(stream), nullptr, 0);
+  hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP), d_verdict,
+                                       c->num_cus, static_cast<hipStream_t>(stream), nullptr, 0, &filt);
   if (e != hipSuccess) return hip_fail(e, "ingress_verify_kernel launch");
   return LNX_OK;
 }

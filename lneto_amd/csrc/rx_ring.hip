@@ -22,6 +22,18 @@
 //     D2H  ok / verdict into pinned result arrays
 // so the copy of batch k+1 overlaps the kernels of batch k: the pipeline runs
 // at the PCIe rate, the kernels are ~100x faster than the link.
+//
+// PCIe bytes: a batch whose frames fill under 90 % of their slots (a realistic
+// length mix: the Zipf mix averages 246 B in 1536-B slots, 6.2x) is packed back
+// to back on the host into the stage's pinned staging with n + 1 offsets, and
+// the kernels run in offsets mode, so the H2D carries the frame bytes plus 8
+// bytes per frame.  lnx_ingress_packets always packs (it gathers the caller's
+// buffers anyway); lnx_egress_packets packs each frame with room for its
+// padding and FCS only, and copies back just that.
+//
+// Stack configuration (lnx_rx_ring_set_filter) and FCS-less devices
+// (LNX_RX_NO_FCS) follow the reference's receive path exactly
+// (ingress_kernel.hip, rx_filter.hpp).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdint>
@@ -30,16 +42,19 @@
 #include <thread>
 #include <vector>
 #include "../../include/lneto_amd.h"
+#include "rx_filter.hpp"
 
 namespace lnx {
 
 int device_resources(const void** image, int* num_cus);
 int hip_error(hipError_t e, const char* what);
+hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                               const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                       uint8_t* ok, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
-                                 uint32_t trim);
+                                 uint32_t trim, const RxFilter* filter);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
@@ -63,25 +78,35 @@ using namespace lnx;
 struct lnx_rx_ring {
   int device = 0;
   uint32_t nslots = 0, cap = 0, batch = 0, depth = 0;
-  uint8_t* h_slots = nullptr;
+  uint8_t* h_slots = nullptr;  // the producer's slots (lnx_rx_ring_slots)
   uint32_t* h_len = nullptr;
-  uint8_t* h_ok = nullptr;
+  uint8_t* h_ok = nullptr;     // per slot: lnx_rx_ring_ingress results
   uint8_t* h_verdict = nullptr;
   struct Stage {
     hipStream_t s = nullptr;
     uint8_t* d_bytes = nullptr;
-    uint64_t* d_start = nullptr;
+    uint64_t* d_start = nullptr;  // slot starts, or the packed batch's offsets (batch + 1)
     uint32_t* d_len = nullptr;
     uint8_t* d_ok = nullptr;
     uint8_t* d_verdict = nullptr;
+    // pinned staging of the packed paths: frame bytes back to back, their
+    // offsets / starts, lengths and results (batch entries each)
+    uint8_t* h_pack = nullptr;
+    uint64_t* h_off = nullptr;
+    uint32_t* h_len = nullptr;
+    uint8_t* h_ok = nullptr;
+    uint8_t* h_verdict = nullptr;
   };
   std::vector<Stage> st;
+  RxFilter filt{};  // lnx_rx_ring_set_filter; on = 0: accept-all
   const void* image = nullptr;
   int num_cus = 0;
-  std::mutex mu;  // one ingress call at a time (the stages are shared)
+  std::mutex mu;  // one call at a time (the stages are shared)
 };
 
 namespace {
+
+using Stage = lnx_rx_ring::Stage;
 
 void ring_free(lnx_rx_ring* r) {
   if (!r) return;
@@ -93,6 +118,11 @@ void ring_free(lnx_rx_ring* r) {
     (void)hipFree(s.d_len);
     (void)hipFree(s.d_ok);
     (void)hipFree(s.d_verdict);
+    (void)hipHostFree(s.h_pack);
+    (void)hipHostFree(s.h_off);
+    (void)hipHostFree(s.h_len);
+    (void)hipHostFree(s.h_ok);
+    (void)hipHostFree(s.h_verdict);
     if (s.s) (void)hipStreamDestroy(s.s);
   }
   (void)hipHostFree(r->h_slots);
@@ -100,70 +130,6 @@ void ring_free(lnx_rx_ring* r) {
   (void)hipHostFree(r->h_ok);
   (void)hipHostFree(r->h_verdict);
   delete r;
-}
-
-// Enqueue slots [b0, b0 + nb) on stage `s` (asynchronous).
-int enqueue(lnx_rx_ring* r, lnx_rx_ring::Stage& s, uint32_t b0, uint32_t nb, uint32_t offset, uint32_t flags) {
-  hipError_t e;
-  const size_t cap = r->cap;
-  if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
-                          s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
-    return hip_error(e, "rx ring H2D");
-  const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
-  hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
-  if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
-  if ((e = launch_fcs_verify_segments(s.d_bytes, s.d_start, s.d_len, nb, s.d_ok, r->image, r->num_cus, s.s)) !=
-      hipSuccess)
-    return hip_error(e, "rx ring FCS verify launch");
-  if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, flags, s.d_verdict, r->num_cus, s.s, s.d_len, 4)) !=
-      hipSuccess)
-    return hip_error(e, "rx ring ingress verify launch");
-  if ((e = hipMemcpyAsync(r->h_ok + b0, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(r->h_verdict + b0, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
-    return hip_error(e, "rx ring D2H");
-  return LNX_OK;
-}
-
-int sync_all(lnx_rx_ring* r) {
-  int rc = LNX_OK;
-  for (auto& s : r->st) {
-    const hipError_t e = hipStreamSynchronize(s.s);
-    if (e != hipSuccess && rc == LNX_OK) rc = hip_error(e, "rx ring hipStreamSynchronize");
-  }
-  return rc;
-}
-
-// Transmit direction, slots [b0, b0 + nb) on stage `s` (asynchronous): the
-// frames (slot[0 : len]) get their checksums (LNX_TX_CHECKSUM) and their
-// padding + FCS (LNX_TX_FCS) on the device, and come back whole with their
-// new lengths; h_verdict = the checksum status, h_ok = the append status.
-int enqueue_tx(lnx_rx_ring* r, lnx_rx_ring::Stage& s, uint32_t b0, uint32_t nb, uint32_t capacity, uint32_t flags) {
-  hipError_t e;
-  const size_t cap = r->cap;
-  if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
-                          s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring H2D");
-  const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
-  hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, 0u);
-  if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
-  if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess || (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring status reset");
-  if ((flags & LNX_TX_CHECKSUM) &&
-      (e = launch_tx_checksum(s.d_bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring checksum launch");
-  if ((flags & LNX_TX_FCS) &&
-      (e = launch_fcs_append(s.d_bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
-          hipSuccess)
-    return hip_error(e, "tx ring FCS append launch");
-  if ((e = hipMemcpyAsync(r->h_slots + (size_t)b0 * cap, s.d_bytes, (size_t)nb * cap, hipMemcpyDeviceToHost,
-                          s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(r->h_len + b0, s.d_len, (size_t)nb * 4, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(r->h_ok + b0, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
-      (e = hipMemcpyAsync(r->h_verdict + b0, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring D2H");
-  return LNX_OK;
 }
 
 // Host copies of a batch, split over up to 16 threads when it is large.
@@ -181,9 +147,95 @@ void parallel_for(uint32_t nb, F&& fn) {
   for (auto& t : th) t.join();
 }
 
-void copy_out(const lnx_rx_ring* r, uint32_t first, uint32_t count, uint8_t* fcs_ok, uint8_t* verdict) {
-  if (fcs_ok) std::memcpy(fcs_ok, r->h_ok + first, count);
-  if (verdict) std::memcpy(verdict, r->h_verdict + first, count);
+// Pack frame j = (ptr(j), len(j)), j < nb, back to back into s.h_pack with
+// offsets s.h_off[0..nb]; returns the packed byte count.
+template <typename Ptr, typename Len>
+uint64_t pack_batch(Stage& s, uint32_t nb, Ptr ptr, Len len) {
+  uint64_t o = 0;
+  for (uint32_t j = 0; j < nb; ++j) {
+    s.h_off[j] = o;
+    o += len(j);
+  }
+  s.h_off[nb] = o;
+  parallel_for(nb, [&](uint32_t a, uint32_t b) {
+    for (uint32_t j = a; j < b; ++j) {
+      const uint64_t l = s.h_off[j + 1] - s.h_off[j];
+      if (l) std::memcpy(s.h_pack + s.h_off[j], ptr(j), l);
+    }
+  });
+  return o;
+}
+
+// Receive direction on stage s (asynchronous), results into ok_dst /
+// verdict_dst (pinned, nb entries).  pack: the frames are packed in s.h_pack
+// (offsets s.h_off[0..nb]); else they sit in whole slots [b0, b0 + nb) of the
+// ring at `offset`.  FCS verify unless LNX_RX_NO_FCS (then fcs_ok = 1 and the
+// verdict covers the whole frame).
+int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, uint32_t offset, uint32_t flags,
+               uint8_t* ok_dst, uint8_t* verdict_dst) {
+  hipError_t e;
+  const bool fcs = !(flags & LNX_RX_NO_FCS);
+  const uint32_t vflags = flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP);
+  const uint32_t trim = fcs ? 4u : 0u;
+  if (pack) {
+    const uint64_t total = s.h_off[nb];
+    if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
+        (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring H2D (packed)");
+    e = fcs ? launch_crc32_frames(s.d_bytes, s.d_start, nb, s.d_ok, true, r->image, r->num_cus, s.s)
+            : hipMemsetAsync(s.d_ok, 1, nb, s.s);
+    if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");
+    if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, nullptr, trim,
+                                   &r->filt)) != hipSuccess)
+      return hip_error(e, "rx ring ingress verify launch");
+  } else {
+    const size_t cap = r->cap;
+    if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
+                            s.s)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring H2D");
+    const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
+    hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
+    e = fcs ? launch_fcs_verify_segments(s.d_bytes, s.d_start, s.d_len, nb, s.d_ok, r->image, r->num_cus, s.s)
+            : hipMemsetAsync(s.d_ok, 1, nb, s.s);
+    if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");
+    if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, s.d_len, trim,
+                                   &r->filt)) != hipSuccess)
+      return hip_error(e, "rx ring ingress verify launch");
+  }
+  if ((e = hipMemcpyAsync(ok_dst, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(verdict_dst, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
+    return hip_error(e, "rx ring D2H");
+  return LNX_OK;
+}
+
+// Transmit direction on stage s (asynchronous): the nb frames packed in
+// s.h_pack at starts s.h_off[j] with lengths s.h_len[j] (each with room for
+// its padding and FCS) get their checksums (LNX_TX_CHECKSUM) and padding + FCS
+// (LNX_TX_FCS) on the device and come back with their new lengths; s.h_verdict
+// = the checksum status, s.h_ok = the append status.
+int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t capacity, uint32_t flags) {
+  hipError_t e;
+  if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
+      (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)nb * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(s.d_len, s.h_len, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring H2D");
+  if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess || (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring status reset");
+  if ((flags & LNX_TX_CHECKSUM) &&
+      (e = launch_tx_checksum(s.d_bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring checksum launch");
+  if ((flags & LNX_TX_FCS) &&
+      (e = launch_fcs_append(s.d_bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
+          hipSuccess)
+    return hip_error(e, "tx ring FCS append launch");
+  if ((total && (e = hipMemcpyAsync(s.h_pack, s.d_bytes, total, hipMemcpyDeviceToHost, s.s)) != hipSuccess) ||
+      (e = hipMemcpyAsync(s.h_len, s.d_len, (size_t)nb * 4, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(s.h_ok, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
+      (e = hipMemcpyAsync(s.h_verdict, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
+    return hip_error(e, "tx ring D2H");
+  return LNX_OK;
 }
 
 }  // namespace
@@ -217,13 +269,21 @@ int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t 
   }
   std::memset(r->h_len, 0, (size_t)nslots * 4);
   r->st.resize(depth);
+  const size_t bb = (size_t)batch_slots * slot_cap;
   for (auto& s : r->st) {
     if ((e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&s.d_bytes), (size_t)batch_slots * slot_cap)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&s.d_start), (size_t)batch_slots * 8)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_bytes), bb)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_start), ((size_t)batch_slots + 1) * 8)) != hipSuccess ||
         (e = hipMalloc(reinterpret_cast<void**>(&s.d_len), (size_t)batch_slots * 4)) != hipSuccess ||
         (e = hipMalloc(reinterpret_cast<void**>(&s.d_ok), batch_slots)) != hipSuccess ||
-        (e = hipMalloc(reinterpret_cast<void**>(&s.d_verdict), batch_slots)) != hipSuccess) {
+        (e = hipMalloc(reinterpret_cast<void**>(&s.d_verdict), batch_slots)) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_pack), bb, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_off), ((size_t)batch_slots + 1) * 8, hipHostMallocDefault)) !=
+            hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_len), (size_t)batch_slots * 4, hipHostMallocDefault)) !=
+            hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_ok), batch_slots, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&s.h_verdict), batch_slots, hipHostMallocDefault)) != hipSuccess) {
       rc = hip_error(e, "rx ring stage allocation");
       ring_free(r);
       return rc;
@@ -238,6 +298,15 @@ void lnx_rx_ring_destroy(lnx_rx_ring* ring) { ring_free(ring); }
 uint8_t* lnx_rx_ring_slots(lnx_rx_ring* ring) { return ring ? ring->h_slots : nullptr; }
 uint32_t* lnx_rx_ring_lengths(lnx_rx_ring* ring) { return ring ? ring->h_len : nullptr; }
 
+int lnx_rx_ring_set_filter(lnx_rx_ring* r, const lnx_rx_filter* filter) {
+  if (!r) return LNX_EINVAL;
+  RxFilter f;
+  if (!rx_filter_of(filter, &f)) return LNX_EINVAL;
+  std::lock_guard<std::mutex> lk(r->mu);
+  r->filt = f;
+  return LNX_OK;
+}
+
 int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t offset, uint32_t flags,
                         uint8_t* fcs_ok, uint8_t* verdict) {
   if (!r) return LNX_EINVAL;
@@ -247,14 +316,85 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
   hipError_t e = hipSetDevice(r->device);
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   int rc = LNX_OK;
+  std::vector<bool> packed_pending(r->depth, false);  // stage k's staging is in use by its last batch
   uint32_t k = 0;
   for (uint32_t b0 = first; b0 < first + count && rc == LNX_OK; b0 += r->batch, ++k) {
     const uint32_t nb = std::min(r->batch, first + count - b0);
-    rc = enqueue(r, r->st[k % r->depth], b0, nb, offset, flags);
+    auto& s = r->st[k % r->depth];
+    auto flen = [&](uint32_t j) -> uint64_t {
+      const uint32_t l = std::min(r->h_len[b0 + j], r->cap);
+      return l > offset ? l - offset : 0u;
+    };
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < nb; ++j) total += flen(j);
+    // whole slots when the frames fill them (no host copy); else frames packed
+    const bool pack = total * 10 < (uint64_t)nb * r->cap * 9;
+    if (pack) {
+      if (packed_pending[k % r->depth] && (e = hipStreamSynchronize(s.s)) != hipSuccess) {
+        rc = hip_error(e, "rx ring hipStreamSynchronize");
+        break;
+      }
+      pack_batch(s, nb, [&](uint32_t j) { return r->h_slots + (size_t)(b0 + j) * r->cap + offset; }, flen);
+    }
+    packed_pending[k % r->depth] = pack;
+    rc = enqueue_rx(r, s, nb, pack, b0, offset, flags, r->h_ok + b0, r->h_verdict + b0);
   }
-  const int rs = sync_all(r);
-  if (rc == LNX_OK) rc = rs;
-  if (rc == LNX_OK) copy_out(r, first, count, fcs_ok, verdict);
+  for (auto& s : r->st) {
+    const hipError_t se = hipStreamSynchronize(s.s);
+    if (se != hipSuccess && rc == LNX_OK) rc = hip_error(se, "rx ring hipStreamSynchronize");
+  }
+  if (rc == LNX_OK) {
+    if (fcs_ok) std::memcpy(fcs_ok, r->h_ok + first, count);
+    if (verdict) std::memcpy(verdict, r->h_verdict + first, count);
+  }
+  return rc;
+}
+
+int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
+                        uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict) {
+  if (!r || (n > 0 && (!bufs || !lens))) return LNX_EINVAL;
+  if (offset >= r->cap) return LNX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)
+    if (lens[i] > r->cap || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
+  if (n == 0) return LNX_OK;
+  std::lock_guard<std::mutex> lk(r->mu);
+  hipError_t e = hipSetDevice(r->device);
+  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
+  // Batches go round-robin over the stages; batch k is packed into the
+  // staging of stage k % depth after that stage's previous batch has drained,
+  // so the gather (host memcpy, parallel) of batch k+1 overlaps the copies
+  // and kernels of batch k.
+  const uint32_t depth = r->depth, per = r->batch;
+  int rc = LNX_OK;
+  std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});  // (first frame, count) per stage
+  auto drain = [&](uint32_t k) {
+    const uint64_t f0 = pending[k].first;
+    const uint32_t cnt = pending[k].second;
+    pending[k].second = 0;
+    const hipError_t se = hipStreamSynchronize(r->st[k].s);
+    if (se != hipSuccess) return hip_error(se, "rx ring hipStreamSynchronize");
+    if (fcs_ok) std::memcpy(fcs_ok + f0, r->st[k].h_ok, cnt);
+    if (verdict) std::memcpy(verdict + f0, r->st[k].h_verdict, cnt);
+    return LNX_OK;
+  };
+  uint64_t i0 = 0;
+  for (uint32_t k = 0; i0 < n && rc == LNX_OK; ++k, i0 += per) {
+    const uint32_t sk = k % depth;
+    if (pending[sk].second) rc = drain(sk);
+    if (rc != LNX_OK) break;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
+    auto& s = r->st[sk];
+    pack_batch(
+        s, nb, [&](uint32_t j) { return bufs[i0 + j] + offset; },
+        [&](uint32_t j) -> uint64_t { return lens[i0 + j] > offset ? lens[i0 + j] - offset : 0u; });
+    rc = enqueue_rx(r, s, nb, true, 0, 0, flags, s.h_ok, s.h_verdict);
+    if (rc == LNX_OK) pending[sk] = {i0, nb};
+  }
+  for (uint32_t k = 0; k < depth; ++k) {
+    if (!pending[k].second) continue;
+    const int d = drain(k);
+    if (rc == LNX_OK) rc = d;
+  }
   return rc;
 }
 
@@ -270,80 +410,26 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   // as lnx_ingress_packets: batches round-robin over the stages, the gather of
   // batch k + 1 and the scatter of batch k - depth + 1 overlap the device work
-  const uint32_t depth = std::min(r->depth, r->nslots);
-  const uint32_t per = std::min(r->batch, r->nslots / depth);
+  const uint32_t depth = r->depth, per = r->batch;
   int rc = LNX_OK;
   std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});
+  // A batch's results reach the caller only from a stream that completed: on
+  // a failed sync its frames, lens and status stay untouched.
   auto drain = [&](uint32_t k) {
-    const hipError_t se = hipStreamSynchronize(r->st[k].s);
-    if (se != hipSuccess) return hip_error(se, "tx ring hipStreamSynchronize");
-    const uint64_t f0 = pending[k].first;
-    const uint32_t cnt = pending[k].second, s0 = k * per;
-    parallel_for(cnt, [&](uint32_t a, uint32_t b) {
-      for (uint32_t j = a; j < b; ++j) {
-        const uint32_t l = r->h_len[s0 + j];
-        if (l) std::memcpy(bufs[f0 + j] + offset, r->h_slots + (size_t)(s0 + j) * r->cap, l);
-        lens[f0 + j] = l;
-        if (status) status[f0 + j] = r->h_verdict[s0 + j] ? r->h_verdict[s0 + j] : r->h_ok[s0 + j];
-      }
-    });
-    pending[k].second = 0;
-    return LNX_OK;
-  };
-  uint64_t i0 = 0;
-  for (uint32_t k = 0; i0 < n && rc == LNX_OK; ++k, i0 += per) {
-    const uint32_t sk = k % depth;
-    if (pending[sk].second) rc = drain(sk);
-    if (rc != LNX_OK) break;
-    const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
-    const uint32_t s0 = sk * per;
-    parallel_for(nb, [&](uint32_t a, uint32_t b) {
-      for (uint32_t j = a; j < b; ++j) {
-        const uint32_t l = lens[i0 + j];
-        if (l) std::memcpy(r->h_slots + (size_t)(s0 + j) * r->cap, bufs[i0 + j] + offset, l);
-        r->h_len[s0 + j] = l;
-      }
-    });
-    rc = enqueue_tx(r, r->st[sk], s0, nb, capacity, flags);
-    pending[sk] = {i0, nb};
-  }
-  for (uint32_t k = 0; k < depth; ++k) {
-    if (!pending[k].second) continue;
-    const int d = drain(k);
-    if (rc == LNX_OK) rc = d;
-  }
-  return rc;
-}
-
-int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32_t* lens, uint64_t n,
-                        uint32_t offset, uint32_t flags, uint8_t* fcs_ok, uint8_t* verdict) {
-  if (!r || (n > 0 && (!bufs || !lens))) return LNX_EINVAL;
-  if (offset >= r->cap) return LNX_EINVAL;
-  for (uint64_t i = 0; i < n; ++i)
-    if (lens[i] > r->cap || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
-  if (n == 0) return LNX_OK;
-  std::lock_guard<std::mutex> lk(r->mu);
-  hipError_t e = hipSetDevice(r->device);
-  if (e != hipSuccess) return hip_error(e, "hipSetDevice");
-  // Batches go round-robin over the stages; batch k gathers into the slot
-  // block of stage k % depth, after that stage's previous batch has drained.
-  // The gather (host memcpy, parallel) of batch k+1 overlaps the copies and
-  // kernels of batch k.  With fewer slots than stages only nslots stages are
-  // used, so every stage's slot block [sk*per, sk*per + per) lies inside the
-  // pinned pool.
-  const uint32_t depth = std::min(r->depth, r->nslots);
-  const uint32_t per = std::min(r->batch, r->nslots / depth);
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  int rc = LNX_OK;
-  std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});  // (first frame, count) per stage
-  auto drain = [&](uint32_t k) {
-    const hipError_t se = hipStreamSynchronize(r->st[k].s);
-    if (se != hipSuccess) return hip_error(se, "rx ring hipStreamSynchronize");
     const uint64_t f0 = pending[k].first;
     const uint32_t cnt = pending[k].second;
-    if (fcs_ok) std::memcpy(fcs_ok + f0, r->h_ok + (size_t)k * per, cnt);
-    if (verdict) std::memcpy(verdict + f0, r->h_verdict + (size_t)k * per, cnt);
     pending[k].second = 0;
+    auto& s = r->st[k];
+    const hipError_t se = hipStreamSynchronize(s.s);
+    if (se != hipSuccess) return hip_error(se, "tx ring hipStreamSynchronize");
+    parallel_for(cnt, [&](uint32_t a, uint32_t b) {
+      for (uint32_t j = a; j < b; ++j) {
+        const uint32_t l = s.h_len[j];
+        if (l) std::memcpy(bufs[f0 + j] + offset, s.h_pack + s.h_off[j], l);
+        lens[f0 + j] = l;
+        if (status) status[f0 + j] = s.h_verdict[j] ? s.h_verdict[j] : s.h_ok[j];
+      }
+    });
     return LNX_OK;
   };
   uint64_t i0 = 0;
@@ -352,25 +438,23 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
     if (pending[sk].second) rc = drain(sk);
     if (rc != LNX_OK) break;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
-    const uint32_t s0 = sk * per;
-    auto gather = [&](uint32_t a, uint32_t b) {
-      for (uint32_t j = a; j < b; ++j) {
-        const uint32_t l = lens[i0 + j];
-        if (l) std::memcpy(r->h_slots + (size_t)(s0 + j) * r->cap, bufs[i0 + j], l);
-        r->h_len[s0 + j] = l;
-      }
-    };
-    const uint32_t nth = nb >= 4096 ? hw : 1;
-    if (nth == 1) {
-      gather(0, nb);
-    } else {
-      std::vector<std::thread> th;
-      for (uint32_t t = 0; t < nth; ++t)
-        th.emplace_back(gather, (uint32_t)((uint64_t)nb * t / nth), (uint32_t)((uint64_t)nb * (t + 1) / nth));
-      for (auto& t : th) t.join();
+    auto& s = r->st[sk];
+    // each frame's room: the frame, then its padding to 60 bytes and the FCS
+    // when they fit `capacity` (else the append leaves it as it is)
+    uint64_t o = 0;
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint32_t l = lens[i0 + j];
+      const uint32_t grown = std::max(l, 60u) + 4u;
+      s.h_off[j] = o;
+      s.h_len[j] = l;
+      o += (flags & LNX_TX_FCS) && grown <= capacity ? grown : l;
     }
-    rc = enqueue(r, r->st[sk], s0, nb, offset, flags);
-    pending[sk] = {i0, nb};
+    parallel_for(nb, [&](uint32_t a, uint32_t b) {
+      for (uint32_t j = a; j < b; ++j)
+        if (s.h_len[j]) std::memcpy(s.h_pack + s.h_off[j], bufs[i0 + j] + offset, s.h_len[j]);
+    });
+    rc = enqueue_tx(r, s, nb, o, capacity, flags);
+    if (rc == LNX_OK) pending[sk] = {i0, nb};
   }
   for (uint32_t k = 0; k < depth; ++k) {
     if (!pending[k].second) continue;

@@ -28,8 +28,8 @@ __device__ __forceinline__ uint16_t fold_sum16(uint32_t sum) {
   return (uint16_t)~(uint16_t)(sum + (sum >> 16));
 }
 
-constexpr int kSumRowLanes = 16;  // one segment per 16-lane row, four per wave
-constexpr int kSumUnroll = 8;     // dwords per lane in flight per batch (512 B per row)
+[[maybe_unused]] constexpr int kSumRowLanes = 16;  // one segment per 16-lane row, four per wave
+[[maybe_unused]] constexpr int kSumUnroll = 8;     // dwords per lane in flight per batch (512 B per row)
 
 __device__ __forceinline__ uint32_t sum_keep_from(int32_t lo) {
   lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);

@@ -193,11 +193,36 @@ def _be16(b: bytes, i: int) -> int:
     return (b[i] << 8) | b[i + 1]
 
 
-def _ipv4_verdict(ip: bytes, flags: int) -> int:
-    """demux4 up to its checksum checks (internet/stack-ip4.go:100-164), with
-    every destination accepted and a handler for every protocol."""
+class StackFilter:
+    """The stack configuration the receive path consults before and between its
+    checksum checks (mirrors lnx_rx_filter, include/lneto_amd.h):
+    StackEthernet's MAC and SetAcceptMulticast (internet/stack-ethernet.go:56-58,
+    146-152) and its handlers by EtherType (RegisterEthernet, :158-161); stackip4's
+    address, SetAcceptMulticast / SetAcceptBroadcast and handlers by protocol
+    (internet/stack-ip4.go:88-93,108-119,135-141); stackip6's address,
+    SetAcceptMulticast6 and handlers (internet/stack-ip6.go:74,93-111)."""
+
+    def __init__(self, mac: bytes, ethertypes=(0x0800, 0x86DD, 0x0806), ip4: bytes = bytes(4),
+                 ip6: bytes = bytes(16), ip4_protocols=(1, 6, 17), ip6_protocols=(6, 17, 58),
+                 eth_accept_multicast=False, ip4_accept_multicast=False, ip4_accept_broadcast=False,
+                 ip6_accept_multicast=False):
+        self.mac, self.ethertypes, self.ip4, self.ip6 = bytes(mac), set(ethertypes), bytes(ip4), bytes(ip6)
+        self.ip4_protocols, self.ip6_protocols = set(ip4_protocols), set(ip6_protocols)
+        self.eth_accept_multicast, self.ip4_accept_multicast = eth_accept_multicast, ip4_accept_multicast
+        self.ip4_accept_broadcast, self.ip6_accept_multicast = ip4_accept_broadcast, ip6_accept_multicast
+
+
+def _ipv4_verdict(ip: bytes, flags: int, filt: StackFilter | None = None) -> int:
+    """demux4 up to its checksum checks (internet/stack-ip4.go:100-164).  With
+    no filter every destination is accepted and every protocol has a handler."""
     if len(ip) < 20:                                   # ipv4.NewFrame (ipv4/frame.go:15-20)
         return ERR_TRUNCATED_FRAME
+    if filt is not None and filt.ip4 != bytes(4) and ip[16:20] != filt.ip4:   # stack-ip4.go:108-119
+        dst = ip[16:20]
+        mc = dst[0] & 0xF0 == 0xE0                     # ipv4.IsMulticast (ipv4/definitions.go:17-19)
+        bc = dst == b"\xff\xff\xff\xff"                # ipv4.IsBroadcast (:34-36)
+        if not (filt.ip4_accept_multicast and mc) and not (filt.ip4_accept_broadcast and bc):
+            return ERR_PACKET_DROP
     # ValidateExceptCRC (ipv4/frame.go:229-238) on a Validator without
     # validateAllowMultiErrors: the first error added wins (validation.go AddError).
     tl, ihl, version = _be16(ip, 2), ip[0] & 0xF, ip[0] >> 4
@@ -218,6 +243,8 @@ def _ipv4_verdict(ip: bytes, flags: int) -> int:
         return ERR_BAD_CRC
     hl, proto = ihl * 4, ip[9]
     payload = ip[hl:tl]                                # Frame.Payload (ipv4/frame.go:188-192)
+    if filt is not None and proto not in filt.ip4_protocols:
+        return ERR_PACKET_DROP                         # nodeByProto nil (stack-ip4.go:135-141)
     if proto == IPPROTO_TCP:
         if ipv4_tcp_pseudo(ip).payload_sum16(payload) != 0:
             return ERR_BAD_CRC
@@ -243,14 +270,19 @@ def _ipv4_verdict(ip: bytes, flags: int) -> int:
     return 0
 
 
-def _ipv6_verdict(ip6: bytes, flags: int = 0) -> int:
+def _ipv6_verdict(ip6: bytes, flags: int = 0, filt: StackFilter | None = None) -> int:
     """demux6 up to its checksum checks (internet/stack-ip6.go:86-138)."""
     if len(ip6) < 40:                                  # ipv6.NewFrame (ipv6/frame.go:13-18)
         return ERR_TRUNCATED_FRAME
+    if filt is not None and filt.ip6 != bytes(16) and ip6[24:40] != filt.ip6:   # stack-ip6.go:93-98
+        if not filt.ip6_accept_multicast or ip6[24] != 0xFF:                    # internal/ip.go:30-35
+            return ERR_PACKET_DROP
     pl = _be16(ip6, 4)
     if pl + 40 > len(ip6):                             # ValidateSize (ipv6/frame.go:123-128)
         return ERR_INVALID_LENGTH_FIELD
     proto = ip6[6]
+    if filt is not None and proto not in filt.ip6_protocols:
+        return ERR_PACKET_DROP                         # nodeByProto nil (stack-ip6.go:107-111)
     payload = ip6[40:40 + pl]                          # Frame.Payload (ipv6/frame.go:34-37)
     if proto == IPPROTO_TCP:
         if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
@@ -279,25 +311,33 @@ def _ipv6_verdict(ip6: bytes, flags: int = 0) -> int:
     return 0
 
 
-def ingress_verdict(frame: bytes, flags: int = 0) -> int:
+def ingress_verdict(frame: bytes, flags: int = 0, filt: StackFilter | None = None) -> int:
     """Checksum-stage verdict of lneto's receive path for one Ethernet frame
     (FCS stripped): StackEthernet.Demux (internet/stack-ethernet.go:139-165)
     size checks, then demux4 / demux6 by EtherType.  0 = every check passed or
     none applies (other EtherTypes); else the errGeneric code returned.
-    Destination filtering and handler lookup (ErrPacketDrop) are stack
-    configuration and are taken as accept-all.  flags: VERIFY_EVIL_BIT,
-    VERIFY_ICMP (ICMP messages also take the ICMP clients' checks)."""
+    filt: the stack's destination and handler configuration (StackFilter), whose
+    ErrPacketDrop checks take the reference's places among the others; None =
+    accept-all.  flags: VERIFY_EVIL_BIT, VERIFY_ICMP (ICMP messages also take
+    the ICMP clients' checks)."""
     if len(frame) < 14:                                # ethernet.NewFrame (ethernet/frame.go:13-18)
         return ERR_TRUNCATED_FRAME
     et = _be16(frame, 12)
+    if filt is not None:                               # stack-ethernet.go:146-152, before ValidateSize
+        dst = frame[0:6]
+        if dst != b"\xff" * 6 and dst != filt.mac:    # ethernet Frame.IsBroadcast (ethernet/frame.go:57-60)
+            if not filt.eth_accept_multicast or dst[0] & 1 == 0:
+                return ERR_PACKET_DROP
     if et <= 1500 and len(frame) < et:                 # ValidateSize (ethernet/frame.go:119-127)
         return ERR_INVALID_LENGTH_FIELD
     if et == ETHERTYPE_VLAN and len(frame) < 18:
         return ERR_TRUNCATED_FRAME
+    if filt is not None and et not in filt.ethertypes:
+        return ERR_PACKET_DROP                         # demuxByProto: no handler (stack-ethernet.go:158-161)
     if et == ETHERTYPE_IPV4:
-        return _ipv4_verdict(frame[14:], flags)
+        return _ipv4_verdict(frame[14:], flags, filt)
     if et == ETHERTYPE_IPV6:
-        return _ipv6_verdict(frame[14:], flags)
+        return _ipv6_verdict(frame[14:], flags, filt)
     return 0
 
 

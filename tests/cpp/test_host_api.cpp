@@ -106,6 +106,56 @@ static void TestAppendFCS() {
   EXPECT(ethernet::CRC32(lneto::Bytes(frame.data(), n)) == LNX_CRC32_RESIDUE, "residue");
 }
 
+// The IPv4/UDP frame of TestRxRing's transmit half, finished (checksums set),
+// to `dst` (MAC) and `ip` (IPv4 destination): 52 bytes, no FCS.
+static std::vector<uint8_t> udpFrame(const uint8_t* dst, const uint8_t* ip) {
+  std::vector<uint8_t> f = {0xc0, 0xff, 0xee, 0, 0xde, 0xad, 0x4e, 0x8b, 0x3a, 0xf9, 0xfb, 0x6b, 0x08, 0x00,
+                            0x45, 0, 0, 38, 0, 1, 0x40, 0, 64, 17, 0, 0, 192, 168, 10, 1, 192, 168, 10, 2,
+                            0x14, 0xe9, 0, 53, 0, 18, 0, 0};
+  for (int i = 0; i < 10; ++i) f.push_back(uint8_t('a' + i));
+  std::memcpy(f.data(), dst, 6);
+  std::memcpy(f.data() + 30, ip, 4);
+  lneto::Bytes iph(f.data() + 14, 20);
+  const uint16_t h = ipv4::CalculateHeaderCRC(iph);
+  f[24] = uint8_t(h >> 8), f[25] = uint8_t(h);
+  lneto::CRC791 c;
+  ipv4::CRCWriteUDPPseudo(iph, c, 18);
+  const uint16_t u = c.PayloadSum16(lneto::Bytes(f.data() + 34, 18));
+  f[40] = uint8_t(u >> 8), f[41] = uint8_t(u);
+  return f;
+}
+
+// The stack filter and an FCS-stripping device through netdev::RxRing
+// (internet/stack-ethernet.go:146-161, internet/stack-ip4.go:108-141): frames
+// for another MAC or IPv4 address, with or without a broken sum, get
+// ErrPacketDrop (2) before the sum is looked at; the stack's own frame passes,
+// and its corrupted copy gets ErrBadCRC (3).
+static void TestRxRingFilter(netdev::RxRing& ring) {
+  const uint8_t us[6] = {0xc0, 0xff, 0xee, 0, 0xde, 0xad}, other[6] = {2, 0xaa, 0xbb, 0xcc, 0xdd, 0xee};
+  const uint8_t ip_us[4] = {192, 168, 10, 2}, ip_other[4] = {192, 168, 10, 77};
+  std::vector<std::vector<uint8_t>> frames = {udpFrame(us, ip_us), udpFrame(other, ip_us), udpFrame(us, ip_other),
+                                              udpFrame(us, ip_us), udpFrame(other, ip_us), udpFrame(us, ip_other)};
+  for (int k = 3; k < 6; ++k) frames[k][50] ^= 0x10;  // a payload byte: the UDP sum fails
+  internet::StackFilter sf;
+  std::memcpy(sf.MAC, us, 6);
+  std::memcpy(sf.Addr4, ip_us, 4);
+  EXPECT(ring.SetFilter(&sf) == LNX_OK, "set filter");
+  ring.SetDeviceStripsFCS(true);
+  std::vector<lneto::Bytes> bufs;
+  for (auto& f : frames) bufs.emplace_back(f.data(), f.size());
+  std::vector<uint8_t> ok, verdict;
+  EXPECT(ring.IngressPackets(bufs, 0, ok, verdict) == LNX_OK, "filtered ingress");
+  const uint8_t want[6] = {0, 2, 2, 3, 2, 2};
+  for (int k = 0; k < 6; ++k) {
+    EXPECT(ok[k] == 1, "no FCS on this device: ok[%d] = %d", k, ok[k]);
+    EXPECT(verdict[k] == want[k], "verdict[%d] = %d, want %d", k, verdict[k], want[k]);
+  }
+  EXPECT(ring.SetFilter(nullptr) == LNX_OK, "accept-all again");
+  EXPECT(ring.IngressPackets(bufs, 0, ok, verdict) == LNX_OK, "accept-all ingress");
+  for (int k = 0; k < 6; ++k) EXPECT(verdict[k] == (k < 3 ? 0 : 3), "accept-all verdict[%d] = %d", k, verdict[k]);
+  ring.SetDeviceStripsFCS(false);
+}
+
 // The receive ring through the C++ mirror: without a GPU it must refuse to
 // open (no silent CPU path); with one, a valid and a corrupted frame.
 static void TestRxRing() {
@@ -146,6 +196,7 @@ static void TestRxRing() {
   ipv4::CRCWriteUDPPseudo(lneto::Bytes(e + 14, 20), c, 18);
   EXPECT(c.PayloadSum16(lneto::Bytes(e + 34, 18)) == 0, "egress UDP CRC verifies");
   EXPECT(buf[0] == 0xEE && buf[1] == 0xEE && buf[2 + 64] == 0xEE, "bytes outside the frame untouched");
+  TestRxRingFilter(ring);
 }
 
 int main() {

@@ -18,11 +18,16 @@ def ether(et: int, payload: bytes) -> bytes:
     return bytes.fromhex("c0ffee00dead") + bytes.fromhex("4e8b3af9fb6b") + struct.pack(">H", et) + payload
 
 
-def ipv4(proto: int, l4: bytes, opts: bytes = b"", flags: int = 0x4000, fix_l4: bool = True) -> bytes:
+IP4_DST = bytes([192, 168, 10, 2])
+IP6_DST = bytes(range(0x30, 0x40))
+
+
+def ipv4(proto: int, l4: bytes, opts: bytes = b"", flags: int = 0x4000, fix_l4: bool = True,
+         dst: bytes = IP4_DST) -> bytes:
     ihl = 5 + len(opts) // 4
     tl = ihl * 4 + len(l4)
     hdr = bytearray(struct.pack(">BBHHHBBH4s4s", 0x40 | ihl, 0, tl, 0x1234, flags, 64, proto, 0,
-                                bytes([192, 168, 10, 1]), bytes([192, 168, 10, 2]))) + opts
+                                bytes([192, 168, 10, 1]), dst)) + opts
     hdr[10:12] = struct.pack(">H", O.ipv4_header_sum16(bytes(hdr)))  # covers 20 bytes only
     l4 = bytearray(l4)
     if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
@@ -39,8 +44,8 @@ def ipv4(proto: int, l4: bytes, opts: bytes = b"", flags: int = 0x4000, fix_l4: 
     return bytes(hdr) + bytes(l4)
 
 
-def ipv6(proto: int, l4: bytes, fix_l4: bool = True) -> bytes:
-    hdr = bytearray(struct.pack(">IHBB", 0x60000000, len(l4), proto, 64)) + bytes(range(0x20, 0x40))
+def ipv6(proto: int, l4: bytes, fix_l4: bool = True, dst: bytes = IP6_DST) -> bytes:
+    hdr = bytearray(struct.pack(">IHBB", 0x60000000, len(l4), proto, 64)) + bytes(range(0x20, 0x30)) + dst
     l4 = bytearray(l4)
     if fix_l4 and proto == O.IPPROTO_TCP and len(l4) >= 18:
         l4[16:18] = b"\0\0"
@@ -271,4 +276,45 @@ def frames(seed: int = 1, count: int = 3000) -> list[bytes]:
             f = ether(0x0800, ipv4(17, udp(b"")))
             f = f + bytes(max(0, 60 - len(f)))
         out.append(f)
+    return out
+
+
+MAC_US = bytes.fromhex("c0ffee00dead")  # ether()'s destination: the stack's own MAC in filter_frames
+
+
+def filter_frames(seed: int = 21, count: int = 2400) -> list[bytes]:
+    """Frames for the stack filter (lnx_rx_filter / oracle.StackFilter): every
+    destination class at each layer (the stack's MAC / broadcast / another
+    unicast MAC / a multicast MAC; the stack's IPv4 address / another / 224/4 /
+    255.255.255.255; the stack's IPv6 address / another / ff02::1), EtherTypes
+    and IP protocols with and without a handler, crossed with broken sums and
+    sizes, so a frame the stack would drop also carries an error that a later
+    check would report (the precedence is the test)."""
+    rng = np.random.default_rng(seed)
+    macs = [MAC_US, b"\xff" * 6, bytes.fromhex("02aabbccddee"), bytes.fromhex("01005e000001")]
+    ip4s = [IP4_DST, bytes([192, 168, 10, 77]), bytes([224, 0, 0, 251]), b"\xff" * 4]
+    ip6s = [IP6_DST, bytes(range(0x50, 0x60)), bytes.fromhex("ff020000000000000000000000000001")]
+    out = []
+    for i in range(count):
+        pay = rng.integers(0, 256, size=int(rng.integers(0, 600)), dtype=np.uint8).tobytes()
+        fam = i % 5
+        if fam in (0, 1):
+            proto = int(rng.choice([6, 17, 1, 47]))
+            l4 = tcp(pay) if proto == 6 else udp(pay) if proto == 17 else icmp(8, pay) if proto == 1 else pay
+            f = ether(0x0800, ipv4(proto, l4, dst=ip4s[int(rng.integers(0, 4))]))
+        elif fam in (2, 3):
+            proto = int(rng.choice([6, 17, 58, 47]))
+            l4 = tcp(pay) if proto == 6 else udp(pay) if proto == 17 else icmp(128, pay) if proto == 58 else pay
+            f = ether(0x86DD, ipv6(proto, l4, dst=ip6s[int(rng.integers(0, 3))]))
+        else:
+            et = int(rng.choice([0x0806, 0x88CC, 0x8100, 46]))
+            f = ether(et, pay + bytes(46))
+        b = bytearray(f)
+        b[0:6] = macs[int(rng.choice(4, p=[0.55, 0.15, 0.15, 0.15]))]
+        r = rng.random()
+        if r < 0.2 and len(b) > 34:          # a broken sum somewhere past the Ethernet header
+            b[int(rng.integers(14, len(b)))] ^= 1 << int(rng.integers(0, 8))
+        elif r < 0.27:                       # a size error
+            b = b[: int(rng.integers(14, max(15, len(b) - 1)))]
+        out.append(bytes(b))
     return out

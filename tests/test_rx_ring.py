@@ -220,3 +220,105 @@ def test_ring_icmp_flag(cuda):
     assert ok.all()
     assert set(want_v.tolist()) >= {0, O.ERR_BAD_CRC, O.ERR_PACKET_DROP, O.ERR_TRUNCATED_FRAME}
     assert np.array_equal(verdict, want_v)
+
+
+def _fill_ring(ring, frames, offset):
+    for i, f in enumerate(frames):
+        ring.slots[i, :offset] = 0xEE
+        ring.slots[i, offset:offset + len(f)] = np.frombuffer(f, dtype=np.uint8)
+        ring.lengths[i] = offset + len(f)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dense", [True, False])
+def test_ring_without_fcs(cuda, dense):
+    """LNX_RX_NO_FCS: a device that strips the FCS (x/netdev/interface.go:34-40)
+    — no FCS check, fcs_ok = 1, verdicts over the whole frame.  dense: frames
+    that fill their slots (whole-slot copies), else a mix packed on the host."""
+    if dense:
+        base = [f for f in G.frames(seed=77, count=3000) if len(f) >= 1000][:400]
+        frames = [f[:1000] for f in base]  # same length: every slot 1000 of 1000 bytes
+    else:
+        frames = G.frames(seed=78, count=1500)
+    offset = 2
+    cap = _cap_for(frames, offset)
+    for how in ("slots", "packets"):
+        ring = L.RxRing(len(frames), slot_cap=cap, batch_slots=256, depth=3)
+        try:
+            if how == "slots":
+                _fill_ring(ring, frames, offset)
+                ok, verdict = ring.ingress(0, len(frames), offset=offset, flags=L.RX_NO_FCS)
+            else:
+                ok, verdict = ring.ingress_packets([b"\xEE" * offset + f for f in frames], offset=offset,
+                                                   flags=L.RX_NO_FCS)
+        finally:
+            ring.close()
+        want = np.array([O.ingress_verdict(f) for f in frames], dtype=np.uint8)
+        assert ok.all(), how
+        bad = np.flatnonzero(verdict != want)
+        assert bad.size == 0, (how, [(int(i), int(verdict[i]), int(want[i])) for i in bad[:10]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("no_fcs", [False, True])
+def test_ring_filter_precedence(cuda, no_fcs):
+    """lnx_rx_ring_set_filter: not-for-us frames (MAC, IPv4 / IPv6 address) and
+    frames without a handler get ErrPacketDrop before or after the other checks
+    as lneto orders them, with and without FCS; set_filter(None) restores accept-all."""
+    from tests.test_rx_filter import _pair
+    ofilt, cfilt = _pair("plain")
+    frames = G.filter_frames(seed=91, count=1800)
+    bufs = frames if no_fcs else [_with_fcs(f) for f in frames]
+    flags = L.VERIFY_ICMP | (L.RX_NO_FCS if no_fcs else 0)
+    ring = L.RxRing(len(bufs), slot_cap=_cap_for(bufs, 0), batch_slots=512, depth=2)
+    try:
+        ring.set_filter(cfilt)
+        ok, verdict = ring.ingress_packets(bufs, offset=0, flags=flags)
+        _fill_ring(ring, bufs, 0)
+        ok2, verdict2 = ring.ingress(0, len(bufs), offset=0, flags=flags)
+        ring.set_filter(None)
+        _, verdict3 = ring.ingress_packets(bufs, offset=0, flags=flags)
+    finally:
+        ring.close()
+    want = np.array([O.ingress_verdict(f, L.VERIFY_ICMP, ofilt) for f in frames], dtype=np.uint8)
+    want_all = np.array([O.ingress_verdict(f, L.VERIFY_ICMP) for f in frames], dtype=np.uint8)
+    assert ok.all() and ok2.all()
+    assert np.array_equal(verdict, want) and np.array_equal(verdict2, want)
+    assert np.array_equal(verdict3, want_all)
+    assert (want == O.ERR_PACKET_DROP).sum() > 400
+
+
+@pytest.mark.gpu
+def test_ring_packed_zipf_lengths(cuda):
+    """Zipf-mix frames (64-1500 B, mean ~246) in 1536-B slots: the batches are
+    packed back to back (PCIe carries the frames, not the slots); every FCS and
+    verdict as the oracle says, including corrupted and empty frames."""
+    from lneto_amd import synth
+    lens = synth.zipf_lengths(6000, seed=5)
+    rng = np.random.default_rng(5)
+    frames = []
+    for i, l in enumerate(lens):
+        f = G.ether(0x0800, G.ipv4(17, G.udp(rng.integers(0, 256, max(0, int(l) - 46), dtype=np.uint8).tobytes())))
+        f = _with_fcs(f)
+        if i % 97 == 0:
+            f = _flip(f, int(rng.integers(0, len(f))))
+        if i % 501 == 0:
+            f = b""
+        frames.append(f)
+    ring = L.RxRing(len(frames), slot_cap=1536, batch_slots=1024, depth=3)
+    try:
+        _fill_ring(ring, frames, 0)
+        ok, verdict = ring.ingress(0, len(frames))
+        ok2, verdict2 = ring.ingress_packets(frames)
+    finally:
+        ring.close()
+    want_ok, want_v = _expect(frames)
+    assert np.array_equal(ok, want_ok) and np.array_equal(ok2, want_ok)
+    assert np.array_equal(verdict, want_v) and np.array_equal(verdict2, want_v)
+    assert (want_ok == 0).sum() >= 60
+
+
+def _flip(f: bytes, i: int) -> bytes:
+    b = bytearray(f)
+    b[i] ^= 0x08
+    return bytes(b)
