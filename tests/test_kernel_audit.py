@@ -54,3 +54,34 @@ def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_loops.py"), str(tmp_path / asm)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def _audit_fixture(tmp_path, name):
+    path = os.path.join(ROOT, "tests", "audit_fixtures", name)
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-c", "--save-temps", "-o",
+                    str(tmp_path / "k.o"), path], cwd=tmp_path, check=True, capture_output=True)
+    asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
+    return subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_loops.py"), str(tmp_path / asm)],
+                          capture_output=True, text=True)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_cross_lane_audit_catches_a_stale_source(tmp_path):
+    """The cross-lane check (a DPP / bpermute / readlane source that some lanes
+    never wrote) flags a register written only under a narrowed exec and
+    passes the same kernel with the register zeroed first."""
+    r = _audit_fixture(tmp_path, "stale_dpp.hip")
+    found = [l for l in r.stdout.splitlines() if "cross-lane" in l]
+    assert len(found) == 1 and found[0].startswith("_Z5stale"), r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_r1g_failing_form_has_no_stale_cross_lane_source(tmp_path):
+    """the round-1 sum16 form that returned wrong sums is
+    caught by the loop-shape check, but none of its cross-lane reads (the
+    row_add16 DPP chain) takes a register some lanes never wrote: the
+    stale-register hypothesis does not explain it."""
+    r = _audit_fixture(tmp_path, "sum16_r1g_divergent.hip")
+    assert any("narrows exec" in l for l in r.stdout.splitlines()), r.stdout
+    assert not any("cross-lane" in l for l in r.stdout.splitlines()), r.stdout
+    assert "8 cross-lane reads checked" in r.stderr

@@ -16,7 +16,19 @@ rows) and multi-dword loads in a wave-uniform loop (the shipped line rows)
 never failed, so neither is flagged; outer grid-stride loops are not
 innermost.
 
-usage: audit_loops.py file.s [symbol-regex]   (exit 1 if any loop is flagged)
+Second check (round 4, the stale-register hypothesis of that failure): every
+CROSS-LANE read -- a DPP operand (quad_perm / row_* / wave_* / row_bcast),
+ds_swizzle_b32, ds_bpermute_b32, v_readlane_b32, v_permlane*_swap -- takes
+values from OTHER lanes, so a source VGPR that some lanes never wrote (they
+were masked off at every write) would hand those lanes' stale contents, left
+by an earlier wave in the same registers, to their neighbours.  Per kernel,
+the audit tracks the exec-mask depth through the linear code (s_and_saveexec /
+s_andn2_saveexec / s_and_b64 exec / s_andn2_b64 exec narrow it, s_or_b64 exec /
+s_mov_b64 exec restore it; the body of a loop whose latch retires lanes counts
+as narrowed) and flags a cross-lane read whose source has no write, anywhere
+before it in the kernel, at an exec depth no narrower than the read's own.
+
+usage: audit_loops.py file.s [symbol-regex]   (exit 1 if any loop or read is flagged)
 """
 import re
 import sys
@@ -61,17 +73,150 @@ def divergent_load_loops(body):
     return found
 
 
+NARROW = re.compile(r"^(s_and_saveexec_b64|s_andn2_saveexec_b64|s_and_b64 exec,|s_andn2_b64 exec,)")
+RESTORE = re.compile(r"^(s_or_b64 exec, exec,|s_mov_b64 exec, s|s_or_saveexec_b64)")
+CROSS = re.compile(r"(quad_perm:|row_shl:|row_shr:|row_ror:|row_mirror|row_half_mirror|row_bcast|wave_shl|wave_rol|"
+                   r"wave_shr|wave_ror|row_newbcast|row_share|row_xmask)|^(ds_swizzle_b32|ds_bpermute_b32|v_readlane_b32|"
+                   r"v_permlane16_swap|v_permlane32_swap)")
+VREG = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+
+
+def regs_of(operand: str):
+    out = set()
+    for m in VREG.finditer(operand):
+        if m.group(1) is not None:
+            out.add(int(m.group(1)))
+        else:
+            out.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def operands(line: str):
+    """(mnemonic, [operand strings]) of an instruction line."""
+    parts = line.split(None, 1)
+    if len(parts) < 2:
+        return parts[0] if parts else "", []
+    ops = [o.strip() for o in re.split(r",(?![^\[]*\])", parts[1])]
+    return parts[0], ops
+
+
+def exec_depths(body):
+    """Exec-narrowing depth of every line (see the module docstring).  An if
+    region opens with s_and_saveexec_b64 sX (or s_and_b64 / s_andn2_b64 exec
+    outside a loop latch) and closes with s_or_b64 exec, exec, sX / s_mov_b64
+    exec, sX: the depth is the count of open regions (a stack of the saved
+    masks; a restore of a mask that is not on it, e.g. the exit of a loop whose
+    latch retired lanes, closes nothing)."""
+    stack, out = [], []
+    for l in body:
+        m = re.match(r"^(s_and_saveexec_b64|s_andn2_saveexec_b64|s_or_saveexec_b64)\s+(s\[\d+:\d+\])", l)
+        r = re.match(r"^(s_or_b64 exec, exec,|s_mov_b64 exec,)\s*(s\[\d+:\d+\])", l)
+        if m and m.group(1) != "s_or_saveexec_b64":
+            stack.append(m.group(2))
+        elif r and r.group(2) in stack:
+            while stack and stack.pop() != r.group(2):
+                pass
+        out.append(len(stack))
+    # the body of an innermost loop that retires lanes at its latch runs narrowed after its first trip
+    labels = {}
+    for i, l in enumerate(body):
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m:
+            labels[m.group(1)] = i
+    for i, l in enumerate(body):
+        m = re.match(r"^s_c?branch\w*\s+(\.LBB\w+)", l)
+        if m and m.group(1) in labels and labels[m.group(1)] <= i:
+            start = labels[m.group(1)]
+            if any(re.match(r"^s_andn2_b64 exec, exec,", t) for t in body[start:i + 1]):
+                for k in range(start, i + 1):
+                    out[k] += 1
+    return out
+
+
+def loop_regions(body):
+    """(first, last) line of every loop (a backward branch and its target label)."""
+    labels = {}
+    for i, l in enumerate(body):
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m:
+            labels[m.group(1)] = i
+    out = []
+    for i, l in enumerate(body):
+        m = re.match(r"^s_c?branch\w*\s+(\.LBB\w+)", l)
+        if m and m.group(1) in labels and labels[m.group(1)] <= i:
+            out.append((labels[m.group(1)], i))
+    return out
+
+
+def vgpr_writes(body, dep):
+    """[(line, reg, exec depth)] of every instruction that writes a VGPR."""
+    out = []
+    for i, l in enumerate(body):
+        if not l or l.startswith(".") or l.endswith(":"):
+            continue
+        mn, ops = operands(l)
+        if not ops:
+            continue
+        if (re.match(r"^(v_|ds_read|ds_bpermute|ds_swizzle|global_load|buffer_load|flat_load|scratch_load)", mn)
+                or re.match(r"^(global_atomic|buffer_atomic|ds_)\w*_rtn", mn)) and not mn.startswith(
+                    ("v_cmp", "v_readfirstlane", "v_readlane")):
+            for r in regs_of(ops[0]):
+                out.append((i, r, dep[i]))
+        elif mn.startswith("v_cmp") and not ops[0].startswith(("s", "vcc")):
+            for r in regs_of(ops[0]):
+                out.append((i, r, dep[i]))
+    return out
+
+
+def stale_cross_lane_reads(body):
+    """[(line, instruction, reg)] of cross-lane reads whose source VGPR has no
+    write at an exec depth <= the read's, before it in the code or anywhere in
+    a loop around it (a loop body laid out after its latch block)."""
+    dep = exec_depths(body)
+    loops = loop_regions(body)
+    writes = {}
+    for i, r, d in vgpr_writes(body, dep):
+        writes.setdefault(r, []).append((i, d))
+    found = []
+    for i, l in enumerate(body):
+        if not CROSS.search(l):
+            continue
+        mn, ops = operands(l)
+        if not ops:
+            continue
+        if mn.startswith("ds_bpermute"):
+            srcs = regs_of(ops[2]) if len(ops) > 2 else set()   # data operand (the address is this lane's)
+        elif mn.startswith("ds_swizzle") or mn.startswith("v_readlane"):
+            srcs = regs_of(ops[1]) if len(ops) > 1 else set()
+        elif mn.startswith("v_permlane"):
+            srcs = regs_of(ops[0]) | regs_of(ops[1])
+        else:  # DPP: the first source operand is the one read from another lane
+            srcs = regs_of(ops[1]) if len(ops) > 1 else set()
+        around = [(a, b) for a, b in loops if a <= i <= b]
+        for r in sorted(srcs):
+            ok = any(d <= dep[i] and (j < i or any(a <= j <= b for a, b in around)) for j, d in writes.get(r, []))
+            if not ok:
+                found.append((i, l, r))
+    return found
+
+
 def main():
     path = sys.argv[1]
     pat = re.compile(sys.argv[2]) if len(sys.argv) > 2 else None
     lines = [l.split(";")[0].strip() for l in open(path).read().split("\n")]
-    bad = 0
+    bad = nread = 0
     for sym, a, b in kernels(lines):
         if pat and not pat.search(sym):
             continue
-        for lab, nl, latch in divergent_load_loops(lines[a:b + 1]):
+        body = lines[a:b + 1]
+        for lab, nl, latch in divergent_load_loops(body):
             print(f"{sym}: loop at {lab} narrows exec and issues {nl} VMEM loads (latch: {latch})")
             bad += 1
+        nread += sum(1 for l in body if CROSS.search(l))
+        for i, l, r in stale_cross_lane_reads(body):
+            print(f"{sym}: cross-lane read of v{r} with no earlier write at its exec depth: {l}")
+            bad += 1
+    print(f"audit: {nread} cross-lane reads checked, {bad} findings", file=sys.stderr)
     sys.exit(1 if bad else 0)
 
 
