@@ -23,6 +23,8 @@ hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* o
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
                               uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
+hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                              const void* image, int num_cus, hipStream_t stream);
 #endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
@@ -116,6 +118,18 @@ std::vector<uint32_t> build_lanes_image() {
 }
 #endif  // LNX_RESEARCH
 
+// The staged lane streams' image (stage_kernel.hip): the slicing-by-2 byte
+// tables A[e] = Z_2(e), B[e] = Z_1(e), then Z_{2^m} as eight nibble tables
+// for m = 0..30, entry (m, i, v) at dword 512 + 128 m + 16 i + v.
+std::vector<uint32_t> build_stage_image() {
+  std::vector<uint32_t> t(512 + 31 * 128);
+  for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 2), t[256 + e] = zshift_bytes(e, 1);
+  for (uint32_t m = 0; m < 31; ++m)
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v) t[512 + 128 * m + 16 * i + v] = zshift_bytes_fast(v << (4 * i), 1ull << m);
+  return t;
+}
+
 // Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
 // byte tables for k = 0..5 (search_kernel.hip).
 // Then the tables of crc32_search_seg_kernel (24-byte lane segments): the
@@ -168,6 +182,7 @@ struct DeviceCtx {
   void* d_image = nullptr;
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
+  uint32_t* d_stage = nullptr;   // crc32_stage_kernel image
 #ifdef LNX_RESEARCH
   // Per-stream scratch of the two-launch TX append (the CRCs between its
   // launches): calls on one stream run in order, so each stream reuses its
@@ -225,8 +240,10 @@ int init_ctx(DeviceCtx& c, int dev) {
   auto fail = [&](hipError_t err, const char* what) {
     (void)hipFree(c.d_image);
     (void)hipFree(c.d_search);
+    (void)hipFree(c.d_stage);
     c.d_image = nullptr;
     c.d_search = nullptr;
+    c.d_stage = nullptr;
     return hip_fail(err, what);
   };
   hipError_t err = hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -240,6 +257,11 @@ int init_ctx(DeviceCtx& c, int dev) {
     return fail(err, "hipMalloc(search tables)");
   if ((err = hipMemcpy(c.d_search, st.data(), st.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
     return fail(err, "hipMemcpy(search tables)");
+  const std::vector<uint32_t> sg = build_stage_image();
+  if ((err = hipMalloc(reinterpret_cast<void**>(&c.d_stage), sg.size() * 4)) != hipSuccess)
+    return fail(err, "hipMalloc(stage image)");
+  if ((err = hipMemcpy(c.d_stage, sg.data(), sg.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(err, "hipMemcpy(stage image)");
   return LNX_OK;
 }
 
@@ -506,8 +528,12 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
-                                      static_cast<hipStream_t>(stream), nullptr);
+  // 300 / 301: the staged lane streams (stage_kernel.hip), CRC / FCS verify
+  hipError_t e = var == 300 || var == 301
+                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var == 301, c->d_stage, c->num_cus,
+                                          static_cast<hipStream_t>(stream))
+                     : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
+                                            static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");
   return LNX_OK;
 }

@@ -1,0 +1,424 @@
+// stage_kernel.hip — batched CRC-32 / FCS verify by staged lane streams, gfx950
+// (round 4).  Reference semantics: ethernet.CRC32 (lneto
+// ethernet/crc.go:19-21) = Go crc32.Checksum(data, IEEETable); the verify mode
+// is the residue form of the FCS check.  The schedule is restated on the host
+// in tests/stage_algebra.py and checked there against zlib.
+//
+// Why: on short frames (the Zipf mix, mean 246 B) every per-frame window
+// layout is bound by the L2 request rate (a line two frames share is asked for
+// twice, a short frame's partial lines cost a request each).
+// Here each line is requested once, whole, and a lane still folds a
+// CONTIGUOUS byte stream, so a frame boundary costs no cross-lane work:
+//
+//  * a wave takes a block of kStageBF consecutive frames, bytes [A, E), and
+//    cuts 64 stretches of Q bytes (Q a multiple of 128) from A rounded down to
+//    128; lane k folds stretch k one dword at a time, r <- Z4(r ^ w), through
+//    lane-private slicing-by-2 tables (Z4 = Z2 o Z2, Z2(v) = (v >> 16) ^
+//    A[v & 0xFF] ^ B[(v >> 8) & 0xFF]; 64 KiB instead of the 128 KiB of
+//    slicing-by-4, which leaves LDS for the staging);
+//  * per round each lane needs its stretch's next 128-byte line: 8
+//    buffer_load_dwordx4, instruction m / lane t reading piece
+//    ((t & 7) - s) & 7 of stretch s = 8 (t >> 3) + m, so every instruction
+//    covers 8 whole lines; the pieces go to the wave's 8 KiB of LDS at
+//    1024 m + 16 t and lane s reads its line back with 8 ds_read_b128 at
+//    1024 (s & 7) + 128 (s >> 3) + 16 ((i + s) & 7), conflict-free;
+//  * a boundary x (an offset of the block) in the dword at 4d, byte c:
+//    e = r ^ (w & lomask(c)), the ending frame's state is Z_c(e) (its CRC the
+//    complement); r <- Z4((w & ~lomask(c)) ^ K_c), K_c = Z_{-c}(~0), is the
+//    new frame's state after the dword from the CRC init.  One boundary per
+//    64-byte half is handled by selects inside the fold; a half where some
+//    lane has two (frames under 64 bytes, empty frames) runs byte by byte;
+//  * a stretch starts inside a frame: its first boundary's state is local.
+//    After the block, P_k (the true register at stretch k's start) is the
+//    previous lane's end register (or, past a frame longer than a stretch,
+//    Z_Q(P_{k-1}) ^ E_{k-1}), and the first frame's state gains Z_d(P_k),
+//    d = x - S_k, by binary powers Z_{2^m} from shared nibble tables.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lnx {
+// research library only until it is measured against the product dispatch
+// (tools/prof/variants.py --var 300)
+#ifdef LNX_RESEARCH
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum class StageMode : int { kCrc = 0, kVerify = 1 };
+
+constexpr int kStageWaves = 8;
+constexpr int kStageThreads = kStageWaves * 64;
+constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
+// LDS layout (bytes)
+constexpr uint32_t kSTab = 0;                               // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
+constexpr uint32_t kSTr = 65536;                            // transposes: 8 KiB per wave
+constexpr uint32_t kSBnd = kSTr + kStageWaves * 8192;       // boundary lists: 1536 B per wave
+constexpr uint32_t kSNib = kSBnd + kStageWaves * 1536;      // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
+constexpr uint32_t kSCtr = kSNib + 31 * 512;                // the workgroup's block counter
+constexpr uint32_t kStageLdsBytes = kSCtr + 16;
+static_assert(kStageLdsBytes <= 163840, "stage LDS");
+// compact image in HBM (api.cpp build_stage_image): A[256], B[256], then the
+// nibble tables verbatim (512 + 31 * 128 dwords)
+
+constexpr uint32_t kSOOB = 0x80000000u;
+constexpr uint32_t kSNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t s_lds(const char* lds, uint32_t a) {
+  return *reinterpret_cast<const uint32_t*>(lds + a);
+}
+// Z_2(v) through the lane-private tables (b0 = this lane's column << 2)
+__device__ __forceinline__ uint32_t s_z2(const char* lds, uint32_t v, uint32_t b0) {
+  const uint32_t a = __builtin_amdgcn_perm(v, b0, 0x0c020400u), b = __builtin_amdgcn_perm(v, b0, 0x0c020500u);
+  return __builtin_amdgcn_bitop3_b32(v >> 16, s_lds(lds, kSTab + a), s_lds(lds, kSTab + b + 128u), 0x96);
+}
+__device__ __forceinline__ uint32_t s_z1(const char* lds, uint32_t v, uint32_t b0) {
+  return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + 128u);
+}
+// Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
+// nibble value picks one of 16 banks, equal values broadcast)
+__device__ __forceinline__ uint32_t s_zpow2(const char* lds, uint32_t m, uint32_t v) {
+  const uint32_t t = kSNib + 512u * m;
+  uint32_t a = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
+  return a;
+}
+// Z_d(v), d < 2^31, by binary powers; lanes whose d is done keep their value
+__device__ __forceinline__ uint32_t s_zd(const char* lds, uint32_t d, uint32_t v) {
+  for (uint32_t m = 0; __builtin_amdgcn_ballot_w64((d >> m) != 0u) != 0; ++m) {
+    const uint32_t z = s_zpow2(lds, m, v);
+    v = ((d >> m) & 1u) ? z : v;
+  }
+  return v;
+}
+
+// K_c = Z_{-c}(0xFFFFFFFF): (w & ~lomask(c)) ^ K_c folded by Z4 is the state,
+// after the dword, of a frame that starts at its byte c
+constexpr uint32_t s_unz(uint32_t v, int nbytes) {
+  for (int i = 0; i < 8 * nbytes; ++i) {
+    const uint32_t b = v >> 31, t = b ? v ^ 0xEDB88320u : v;
+    v = (t << 1) | b;
+  }
+  return v;
+}
+constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
+
+template <StageMode MODE>
+__global__ void __launch_bounds__(kStageThreads, 1)
+crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
+                   uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char lds[kStageLdsBytes];
+  // ---- image: A / B values expanded into their 32 bank columns, nibble tables verbatim
+  {
+    const uint32_t t = threadIdx.x;  // 512 threads: one A or B value each
+    const uint32_t v = image[t];
+    const uint32_t m = t >> 8, e = t & 255u;
+    uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
+    const uint4 v4 = {v, v, v, v};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+    for (uint32_t i = t; i < 31u * 128u; i += kStageThreads)
+      reinterpret_cast<uint32_t*>(lds + kSNib)[i] = image[512 + i];
+    if (t == 0) *reinterpret_cast<uint32_t*>(lds + kSCtr) = 0;
+  }
+  __syncthreads();
+  const uint64_t fb0 = (uint64_t)blockIdx.x * frames_per_wg;
+  if (fb0 >= nframes) return;
+  const uint64_t fb1 = fb0 + frames_per_wg < nframes ? fb0 + frames_per_wg : nframes;
+  const uint32_t nslice = (uint32_t)(fb1 - fb0);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t b0 = (lane & 31u) << 2;
+  char* tr = lds + kSTr + 8192u * wv;
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kSBnd + 1536u * wv);
+  constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
+  const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<char*>(out) + fb0 * elem, (short)0, (int)(nslice * elem), 0x00020000);
+  // this lane's read-back addresses: piece i of its line at rb + 16 ((i + lane) & 7)
+  const uint32_t rb = 1024u * (lane & 7u) + 128u * (lane >> 3), rot = lane & 7u;
+
+  for (;;) {
+    uint32_t blk = 0;
+    if (lane == 0) blk = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kSCtr), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+    blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk);
+    const uint64_t f0r = (uint64_t)blk * kStageBF;  // relative to fb0
+    if (f0r >= nslice) break;
+    const uint32_t bf = (uint32_t)(nslice - f0r < kStageBF ? nslice - f0r : kStageBF);
+    const uint64_t f0 = fb0 + f0r;
+    const uint64_t A = off[f0], E = off[f0 + bf];
+    const uint8_t* pa = bytes + A;
+    const uint32_t adj = (uint32_t)(reinterpret_cast<uintptr_t>(pa) & 127u);
+    const uint64_t span = E > A ? E - A + adj : adj;
+    // ---- boundary list (relative to the line-aligned base): x_j = off[f0 + j] - A + adj
+#pragma unroll
+    for (uint32_t i = 0; i < 6u; ++i) {  // (six whole-wave loads: entry j > bf re-reads entry bf)
+      const uint32_t j = lane + 64u * i;
+      const uint64_t o = off[f0 + (j <= bf ? j : bf)];
+      const uint32_t x = o > A ? (uint32_t)(o - A) + adj : adj;  // (non-decreasing offsets: o >= A)
+      list[j] = j <= bf ? x : kSNone;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (span >= (1ull << 31) - 65536) {
+      // gigabyte frames: byte-serial fold per frame, one lane per frame
+      // (the byte loop runs with the whole wave active: a lane past its frame
+      // re-reads byte A and keeps its register, so no load issues under
+      // narrowed exec — the audit's loop rule)
+      for (uint32_t j0 = 0; j0 < bf; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        uint32_t r = 0xFFFFFFFFu;
+        const uint64_t s = j < bf ? off[f0 + j] : A, e0 = j < bf ? off[f0 + j + 1] : A;
+        const uint64_t e = e0 > s ? e0 : s;
+        for (uint64_t q = s;; ++q) {
+          const bool act = q < e;
+          if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+          const uint32_t b = bytes[act ? q : A];
+          const uint32_t nr = s_z1(lds, r ^ b, b0);
+          r = act ? nr : r;
+        }
+        if (j < bf) {
+          const uint32_t crc = ~r;
+          const uint32_t v = MODE == StageMode::kCrc ? crc : (uint32_t)(e - s >= 4 && crc == 0x2144DF1Cu);
+          if (MODE == StageMode::kCrc)
+            __builtin_amdgcn_raw_buffer_store_b32(v, out_rsrc, (uint32_t)(f0r + j) * 4u, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, (uint32_t)(f0r + j), 0, 0);
+        }
+      }
+      continue;
+    }
+    const uint32_t sp = (uint32_t)span;
+    uint32_t Q = ((sp + 63u) / 64u + 127u) & ~127u;
+    Q = Q < 128u ? 128u : Q;
+    const uint32_t rounds = Q / 128u;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pa - adj), (short)0, (int)sp, 0x00020000);
+    // ---- this lane's stretch [Sk, Sk + Q) and its first boundary j = lower_bound(list, Sk)
+    const uint32_t Sk = lane * Q;
+    uint32_t lo = 0, hi = bf + 1u;
+    while (__builtin_amdgcn_ballot_w64(lo < hi) != 0) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint32_t xm = list[mid < 383u ? mid : 383u];
+      if (lo < hi) {
+        if (xm >= Sk) hi = mid; else lo = mid + 1u;
+      }
+    }
+    const uint32_t jstart = lo;
+    uint32_t j = lo;
+    uint32_t x = list[j], x1 = list[j + 1u];
+    uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
+    uint32_t r = 0;
+    bool first = true;
+    uint32_t rec_j = 0, rec_S = 0, rec_d = 0;  // the first boundary's frame (carry pending)
+    bool rec = false;
+    // load offsets: instruction m reads stretch s = 8 (lane >> 3) + m, piece ((lane & 7) - s) & 7
+    uint32_t lo_m[8];
+#pragma unroll
+    for (uint32_t m = 0; m < 8; ++m) {
+      const uint32_t s = 8u * (lane >> 3) + m;
+      lo_m[m] = s * Q + 16u * (((lane & 7u) - s) & 7u);
+    }
+    // Streaming loads are inline asm (hipcc neither counts them nor merges
+    // their waits across the fold's branches into vmcnt(0)): every round
+    // issues exactly 8 of them (rounds past the stretch get an offset past
+    // the range: no memory traffic) after exactly 2 result stores, so the wait
+    // for a slot is a static vmcnt(10).  The statement opens with s_nop 4 (a
+    // descriptor SGPR restored by VALU needs 5 wait states before a VMEM
+    // instruction reads it), outputs early-clobber.
+    auto issue = [&](u32x4(&b)[8], uint32_t rr) {
+      const uint32_t so = rr < rounds ? rr * 128u : kSOOB;
+      asm volatile(
+          "s_nop 4\n\t"
+          "buffer_load_dwordx4 %0, %8, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %1, %9, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %2, %10, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %3, %11, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %4, %12, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %5, %13, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %6, %14, %16, %17 offen\n\t"
+          "buffer_load_dwordx4 %7, %15, %16, %17 offen"
+          : "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]), "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6]), "=&v"(b[7])
+          : "v"(lo_m[0]), "v"(lo_m[1]), "v"(lo_m[2]), "v"(lo_m[3]), "v"(lo_m[4]), "v"(lo_m[5]), "v"(lo_m[6]),
+            "v"(lo_m[7]), "s"(rs), "s"(so));
+    };
+    // results of the fast halves, held to the next round's flush (one per half)
+    uint32_t hv0 = 0, hf0 = kSOOB, hv1 = 0, hf1 = kSOOB;
+    auto store = [&](uint32_t v, uint32_t at) {
+      if constexpr (MODE == StageMode::kCrc)
+        __builtin_amdgcn_raw_buffer_store_b32(v, out_rsrc, at, 0, 0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, at, 0, 0);
+    };
+    // exactly two stores per flush, in asm so that hipcc cannot merge or drop
+    // them (the ring's vmcnt(10) counts them)
+    auto flush = [&]() {
+      if constexpr (MODE == StageMode::kCrc)
+        asm volatile("buffer_store_dword %0, %1, %4, 0 offen\n\tbuffer_store_dword %2, %3, %4, 0 offen"
+                     ::"v"(hv0), "v"(hf0), "v"(hv1), "v"(hf1), "s"(out_rsrc) : "memory");
+      else
+        asm volatile("buffer_store_byte %0, %1, %4, 0 offen\n\tbuffer_store_byte %2, %3, %4, 0 offen"
+                     ::"v"(hv0), "v"(hf0), "v"(hv1), "v"(hf1), "s"(out_rsrc) : "memory");
+      hf0 = hf1 = kSOOB;
+    };
+    // the end of the frame at boundary j (state S, at position xe): a result,
+    // or the stretch's first frame, held until the carries are known; the
+    // result goes to the half's hold (slot h) or, in a byte-serial half, out at once
+    auto end_at = [&](bool ev, uint32_t S, uint32_t xe, int h) {
+      const bool is_first = ev && first && j > 0;
+      rec_j = is_first ? j : rec_j;
+      rec_S = is_first ? S : rec_S;
+      rec_d = is_first ? xe - Sk : rec_d;
+      rec = rec || is_first;
+      const bool res = ev && !first && j > 0;
+      first = ev ? false : first;
+      const uint32_t crc = ~S;
+      const uint32_t fr = (uint32_t)f0r + j - 1u;
+      const uint32_t val = MODE == StageMode::kCrc ? crc : ((xe - xprev >= 4u && crc == 0x2144DF1Cu) ? 1u : 0u);
+      const uint32_t at = res ? fr * elem : kSOOB;
+      if (h == 0) {
+        hv0 = res ? val : hv0, hf0 = res ? at : hf0;
+      } else if (h == 1) {
+        hv1 = res ? val : hv1, hf1 = res ? at : hf1;
+      } else {
+        store(val, at);
+      }
+    };
+    auto advance = [&](bool ev) {
+      xprev = ev ? x : xprev;
+      j = ev ? j + 1u : j;
+      x = ev ? x1 : x;
+      const uint32_t x2 = list[j + 1u < 383u ? j + 1u : 383u];
+      x1 = ev ? x2 : x1;
+    };
+
+    // one round: wait for the slot, stage its pieces in LDS, flush the held
+    // results, refill the slot two rounds ahead, fold the lane's line in two
+    // 64-byte halves
+    auto round_step = [&](u32x4(&cur)[8], uint32_t rr) {
+      asm volatile("s_waitcnt vmcnt(10)"
+                   : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
+                     "+v"(cur[6]), "+v"(cur[7]));
+#pragma unroll
+      for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
+      flush();
+      issue(cur, rr + 2u);
+#pragma unroll
+      for (uint32_t h = 0; h < 2; ++h) {
+        u32x4 q[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t pi = 4u * h + i;
+          q[i] = *reinterpret_cast<const u32x4*>(tr + rb + 16u * ((pi + rot) & 7u));
+        }
+        const uint32_t P = Sk + 128u * rr + 64u * h;
+        const uint32_t rel = x - P;
+        const bool in = rel < 64u;
+        if (__builtin_amdgcn_ballot_w64(x1 - P < 64u) != 0) {
+          // two or more boundaries in some lane's half (frames under 64
+          // bytes): byte by byte, the bytes re-read from the staged line (a
+          // rolled loop: this path is rare and must not bloat the fast one)
+#pragma nounroll
+          for (uint32_t b = 0; b < 64u; ++b) {
+            const uint32_t pi = 4u * h + (b >> 4);
+            const uint32_t w = s_lds(tr, rb + 16u * ((pi + rot) & 7u) + (b & 12u));
+            const uint32_t pos = P + b;
+            while (__builtin_amdgcn_ballot_w64(x == pos) != 0) {
+              const bool ev = x == pos;
+              end_at(ev, r, x, 2);
+              r = ev ? 0xFFFFFFFFu : r;
+              advance(ev);
+            }
+            r = s_z1(lds, r ^ (w >> (8u * (b & 3u))), b0);
+          }
+          continue;
+        }
+        const uint32_t kb = in ? rel >> 2 : 99u, c = rel & 3u;
+        const uint32_t lm = in ? (uint32_t)((1ull << (8u * c)) - 1ull) : 0u;
+        const uint32_t Kc = c == 0u ? 0xFFFFFFFFu : c == 1u ? kK1 : c == 2u ? kK2 : kK3;
+        uint32_t ecap = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 16; ++d) {
+          const uint32_t w = q[d >> 2][d & 3u];
+          const bool at = d == kb;
+          ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
+          const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
+          const uint32_t v = at ? vr : r ^ w;
+          r = s_z2(lds, s_z2(lds, v, b0), b0);
+        }
+        if (__builtin_amdgcn_ballot_w64(in) != 0) {
+          uint32_t S = ecap;  // Z_c(e), c = 0..3
+#pragma unroll
+          for (uint32_t s = 0; s < 3; ++s) {
+            const uint32_t z = s_z1(lds, S, b0);
+            S = s < c ? z : S;
+          }
+          end_at(in, S, x, (int)h);
+          advance(in);
+        }
+      }
+    };
+    u32x4 buf0[8], buf1[8];
+    flush();  // (two stores, so that the first waits count alike)
+    issue(buf0, 0);
+    flush();
+    issue(buf1, 1);
+    for (uint32_t rr = 0; rr < rounds; rr += 2) {
+      round_step(buf0, rr);
+      if (rr + 1u < rounds) round_step(buf1, rr + 1u);
+    }
+    flush();
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(buf0[0]), "+v"(buf0[1]), "+v"(buf0[2]), "+v"(buf0[3]), "+v"(buf0[4]),
+                 "+v"(buf0[5]), "+v"(buf0[6]), "+v"(buf0[7]));
+    asm volatile("" : "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]), "+v"(buf1[4]), "+v"(buf1[5]),
+                 "+v"(buf1[6]), "+v"(buf1[7]));
+    // ---- carries: the true register at each stretch's start
+    const uint32_t E1 = r;
+    const bool hb = j > jstart;  // this stretch holds a boundary
+    const uint32_t up = ((lane + 63u) & 63u) << 2;
+    const uint32_t Ep = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)E1);
+    const bool hbp = lane == 0 || __builtin_amdgcn_ds_bpermute((int)up, (int)hb) != 0;
+    uint32_t Pk = Ep;
+    if (__builtin_amdgcn_ballot_w64(rec && !hbp) != 0) {
+      // a frame longer than a stretch: P_k = Z_Q(P_{k-1}) ^ E_{k-1} through
+      // stretches without a boundary (Jacobi sweeps until nothing changes)
+      for (uint32_t it = 0; it < 64u; ++it) {
+        const uint32_t Pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)Pk);
+        const uint32_t zq = s_zd(lds, hbp ? 0u : Q, Pp);
+        const uint32_t Pn = hbp ? Ep : zq ^ Ep;
+        const bool ch = Pn != Pk;
+        Pk = Pn;
+        if (__builtin_amdgcn_ballot_w64(ch) == 0) break;
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(rec) != 0) {
+      const uint32_t S = rec_S ^ s_zd(lds, rec ? rec_d : 0u, Pk);
+      const uint32_t crc = ~S;
+      const uint32_t fr = (uint32_t)f0r + rec_j - 1u;
+      if constexpr (MODE == StageMode::kCrc) {
+        __builtin_amdgcn_raw_buffer_store_b32(crc, out_rsrc, rec ? fr * 4u : kSOOB, 0, 0);
+      } else {
+        const uint32_t xa = list[rec_j > 0 ? rec_j - 1u : 0u], xe = list[rec_j];
+        const uint32_t ok = (xe - xa >= 4u && crc == 0x2144DF1Cu) ? 1u : 0u;
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)ok, out_rsrc, rec ? fr : kSOOB, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next block
+  }
+}
+
+hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                              const void* image, int num_cus, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t grid = (n + kStageBF - 1) / kStageBF;
+  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+  const uint64_t per = (n + grid - 1) / grid;
+  const uint32_t* img = static_cast<const uint32_t*>(image);
+  if (verify)
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3((unsigned)grid), dim3(kStageThreads), 0, stream,
+                       bytes, off, n, per, img, out);
+  else
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3((unsigned)grid), dim3(kStageThreads), 0, stream,
+                       bytes, off, n, per, img, out);
+  return hipGetLastError();
+}
+
+#endif  // LNX_RESEARCH
+}  // namespace lnx
