@@ -1526,10 +1526,10 @@ template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int 
           int KSL = 13, int LWL = 2, bool LJM = true, int LEP = 1, bool REDGE = true, int NSR4 = 4, int NW4 = 1,
           int STR = 0>
 __global__ void __launch_bounds__(kBlockThreads, 1)
-crc32_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
+crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the FCS through it */ const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
                   uint64_t* __restrict__ timeline,
-                  const uint32_t* __restrict__ seg_len, uint32_t cap) {
+                  const uint32_t* seg_len, uint32_t cap) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path

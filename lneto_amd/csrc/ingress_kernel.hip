@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 #include "rx_filter.hpp"
 
 namespace lnx {
@@ -94,9 +95,13 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
 // zeroed); lanes 0..7 of the row then store the 2-byte fields (IPv4 total
 // length / IPv6 payload length, header CRC, transport CRC, UDP length) and
 // `verdict` receives the status (0, or 18 / 15 with the frame untouched).
+// (the generate form writes the frames: its byte pointer is not const)
+template <bool GEN>
+using IngBytes = std::conditional_t<GEN, uint8_t, const uint8_t>;
+
 template <int UNR, bool QW, bool GEN = false>
 __global__ void __launch_bounds__(kIngBlock)
-ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
+ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
                       uint32_t trim, RxFilter filt) {
   static_assert(!GEN || QW, "generate runs on the qword rows");
@@ -114,7 +119,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     const uint64_t e = !live ? 0 : (seg_len ? s + (sl > trim ? sl - trim : 0u) : (e1 > s + trim ? e1 - trim : s));
     const uint64_t len64 = e > s ? e - s : 0;
     const uint32_t L = len64 < 0x7FFFFFFFull ? (uint32_t)len64 : 0x7FFFFFFFu;
-    const uint8_t* fr = bytes + s;
+    IngBytes<GEN>* fr = bytes + s;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & (QW ? 7u : 3u));
     const uint32_t* base = reinterpret_cast<const uint32_t*>(fr - mis);
     // dword k of base holds frame offsets 4k - mis .. 4k - mis + 3
@@ -512,7 +517,7 @@ ingress_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
       const uint32_t fo = k == 0 ? g_off[0] : k == 1 ? g_off[1] : k == 2 ? g_off[2] : g_off[3];
       const uint32_t fv = k == 0 ? g_val[0] : k == 1 ? g_val[1] : k == 2 ? g_val[2] : g_val[3];
       if (live && v == 0 && k < 4 && fo != 0) {
-        uint8_t* q = const_cast<uint8_t*>(fr) + fo;
+        uint8_t* q = fr + fo;
         if ((reinterpret_cast<uintptr_t>(q) & 1u) == 0) {
           *reinterpret_cast<uint16_t*>(q) = (uint16_t)(((fv & 0xFFu) << 8) | ((fv >> 8) & 0xFFu));
         } else {
