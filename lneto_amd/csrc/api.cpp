@@ -138,7 +138,7 @@ std::vector<uint32_t> build_stage_image() {
 // then Z_{48*2^k} for k = 0..4 (crc32_search_half_kernel, 48-byte segments).
 std::vector<uint32_t> build_search_tables() {
   constexpr uint32_t kOld = 256 + 6 * 1024, kSeg = 24;  // = kSearchSeg
-  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024 + 4096 + 1024);
+  std::vector<uint32_t> t(kOld + 8192 + 7 * 1024 + 5 * 1024 + 4096 + 1024 + 4096 + 3 * 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 1);
   for (uint32_t k = 0; k < 6; ++k)
     for (uint32_t m = 0; m < 4; ++m)
@@ -164,6 +164,16 @@ std::vector<uint32_t> build_search_tables() {
   // Z_24 as four byte tables (crc32_search_u_kernel's split chains: half a 48-byte segment)
   for (uint32_t m = 0; m < 4; ++m)
     for (uint32_t e = 0; e < 256; ++e) t[kOld + 8192 + 12 * 1024 + 4096 + m * 256 + e] = zshift_bytes(e << (8 * m), 24);
+  // octet segments (crc32_search_o_kernel): Z_48 as eight nibble tables in 32
+  // bank columns, (i, v, c) at (16 i + v) * 32 + c, then Z_{192*2^k}, k = 0..2
+  constexpr uint32_t kOct = kOld + 8192 + 12 * 1024 + 4096 + 1024;
+  for (uint32_t i = 0; i < 8; ++i)
+    for (uint32_t v = 0; v < 16; ++v)
+      for (uint32_t c = 0; c < 32; ++c) t[kOct + (16 * i + v) * 32 + c] = zshift_bytes_fast(v << (4 * i), 48);
+  for (uint32_t k = 0; k < 3; ++k)
+    for (uint32_t m = 0; m < 4; ++m)
+      for (uint32_t e = 0; e < 256; ++e)
+        t[kOct + 4096 + k * 1024 + m * 256 + e] = zshift_bytes_fast(e << (8 * m), (uint64_t)192 << k);
   return t;
 }
 

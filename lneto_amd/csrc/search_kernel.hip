@@ -747,6 +747,175 @@ crc32_search_u_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     search_u_body<NC, SPLIT, GLD>(lds, bytes, off, min_off, n, tables, result);
 }
 
+// Octet segments (round 4; LNX_PROF_SEARCH=o in the research library).  The
+// shared-table lookups (the scan, 5 levels over 32 lanes, 0.5 lookups per byte
+// with about 2.6x bank conflicts) were 22 % of the product's LDS cycles.  Here
+// 8 lanes take a capture's 1536-byte block, 192 bytes each, so a wave folds 8
+// captures and the scan has 3 levels over 8 lanes (0.06 shared lookups per
+// byte).  Each lane's 192 bytes are four 48-byte chains folded side by side
+// (the same dependent-chain length as the product's 12 words):
+//   pass A   la_c = chain c folded from 0 (U layout, conflict-free)
+//            l = Z48(Z48(Z48(la_0) ^ la_1) ^ la_2) ^ la_3   (Horner)
+//   scan     Z_{192*2^k}, k = 0..2, shared byte tables (lane 0 folds Z_192(carry))
+//   entries  r_0 = register entering the segment, r_{c+1} = Z48(r_c) ^ la_c
+//   pass B   word checks on the four chains side by side
+// Z48 goes through lane-private nibble tables (8 conflict-free lookups, 16 KiB
+// in 32 bank columns).  A lane keeps its smallest valid hit byte; the first
+// lane of its octet with a hit gives the capture's answer (lanes are in byte
+// order).  tests/test_search_algebra.py::oct_search restates the schedule.
+constexpr uint32_t kOctNibOff = kZ24Off + 1024;          // host tables: Z_48 nibble tables, 32 columns
+[[maybe_unused]] constexpr uint32_t kOctLevOff = kOctNibOff + 4096;  // host tables: Z_{192*2^k}, k = 0..2 (copied with the nibbles)
+constexpr uint32_t kOctLdsDwords = 32768 + 4096 + 3 * 1024;
+static_assert(kOctLdsDwords * 4 <= 163840, "octet LDS");
+
+#ifdef LNX_RESEARCH
+__global__ void __launch_bounds__(kSegBlock, 1)
+crc32_search_o_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                      const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
+                      int64_t* __restrict__ result) {
+  constexpr uint32_t LPC = 8, SEG = 1536 / LPC, NW = SEG / 4, CW = 12, NCH = NW / CW;
+  static_assert(NCH == 4, "four 48-byte chains");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[kOctLdsDwords];
+  {
+    static_assert(kSegBlock == 1024, "one U value per thread");
+    const uint32_t t = threadIdx.x, v = tables[kSegTabOff + 8192 + 6 * 1024 + t];
+    const uint32_t ua = ((t >> 9) << 16) | ((t & 255u) << 8) | (((t >> 8) & 1u) << 7);
+    uint4* row = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds) + ua);
+    const uint4 v4 = {v, v, v, v};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+  }
+  for (uint32_t i = threadIdx.x; i < 4096u + 3u * 1024u; i += kSegBlock) lds[32768 + i] = tables[kOctNibOff + i];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63u, col = lane & 31u, hl = lane & (LPC - 1), oct = lane / LPC;
+  const uint32_t* zt = lds + 32768 + 4096;  // Z_{192*2^k} at zt + 1024 k (shared)
+  const uint32_t ub0 = col << 2, ub1 = ub0 | 65536u;
+  // Z48 through the lane-private nibble tables: (i, v) at byte ((16 i + v) << 7) + 4 col
+  const char* nib = reinterpret_cast<const char*>(lds + 32768) + ub0;
+  auto z48 = [&](uint32_t x) -> uint32_t {
+    uint32_t y[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+      y[i] = *reinterpret_cast<const uint32_t*>(nib + ((16u * i + __builtin_amdgcn_ubfe(x, 4 * i, 4)) << 7));
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(y[0], y[1], y[2], 0x96),
+                                       __builtin_amdgcn_bitop3_b32(y[3], y[4], y[5], 0x96), y[6] ^ y[7], 0x96);
+  };
+  const uint64_t nwaves = (uint64_t)gridDim.x * (kSegBlock / 64);
+  for (uint64_t q = (uint64_t)blockIdx.x * (kSegBlock / 64) + (threadIdx.x >> 6); q * (64 / LPC) < n; q += nwaves) {
+    const uint64_t ga = q * (64 / LPC);
+    const uint64_t c = ga + oct;
+    const bool live = c < n;
+    const uint64_t s = live ? off[c] : 0, e = live ? off[c + 1] : 0;
+    const int64_t L = e > s ? (int64_t)(e - s) : 0;
+    int64_t m = live && min_off ? min_off[c] : 0;
+    if (m < 0) m = 0;
+    int64_t found = -1;
+    bool act = live && L >= m + 4;
+    uint32_t carry = 0xFFFFFFFFu;
+    // the group's bytes through one descriptor when every capture lies inside [off[ga], off[gb])
+    const uint64_t gb = ga + 64 / LPC < n ? ga + 64 / LPC : n;
+    auto uni64 = [](uint64_t x) -> uint64_t {
+      return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
+    };
+    const uint64_t gs = uni64(off[ga]), ge = uni64(off[gb]);
+    const bool inside = ge >= gs && ge - (gs & ~3ull) + 3 < (1ull << 31) && (e <= s || (s >= gs && e <= ge));
+    const bool gfast = __builtin_amdgcn_ballot_w64(!inside) == 0;
+    const uint64_t gbase = gs & ~3ull;
+    const __amdgpu_buffer_rsrc_t grsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(bytes + gbase), (short)0, gfast ? (int)((ge - gbase + 3) & ~3ull) : 0, 0x00020000);
+    for (int64_t B = 0; __builtin_amdgcn_ballot_w64(act) != 0; B += LPC * SEG) {
+      const int64_t base = B + (int64_t)(SEG * hl);
+      const uint32_t sh = (uint32_t)((s + (uint64_t)base) & 3u);
+      uint32_t u[NW];
+      {
+        uint32_t v[NW + 1];
+        if (gfast) {
+          const uint32_t vo = act ? (uint32_t)(((s + (uint64_t)base) & ~3ull) - gbase) : 0x80000000u;
+#pragma unroll
+          for (uint32_t i = 0; i <= NW; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b32(grsrc, vo + 4 * i, 0, 0);
+        } else {
+          const uint8_t* dj = bytes + s;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(dj + base - sh);
+          const int64_t nd64 = act ? (L - base + (int64_t)sh + 3) >> 2 : 0;
+          const int32_t nd = nd64 < 0 ? 0 : (nd64 > (int64_t)(NW + 1) ? (int32_t)(NW + 1) : (int32_t)nd64);
+#pragma unroll
+          for (uint32_t i = 0; i <= NW; ++i) v[i] = (int32_t)i < nd ? wp[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < NW; ++i) u[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sh);
+      }
+      // pass A: the four chains side by side
+      uint32_t x[NCH], la[NCH];
+#pragma unroll
+      for (uint32_t ch = 0; ch < NCH; ++ch) x[ch] = u[CW * ch];
+#pragma unroll
+      for (uint32_t i = 0; i + 1 < CW; ++i)
+#pragma unroll
+        for (uint32_t ch = 0; ch < NCH; ++ch) x[ch] = ustep_xor(lds, x[ch], u[CW * ch + i + 1], ub0, ub1);
+#pragma unroll
+      for (uint32_t ch = 0; ch < NCH; ++ch) la[ch] = ustep_xor(lds, x[ch], 0u, ub0, ub1);
+      uint32_t P = la[0];
+#pragma unroll
+      for (uint32_t ch = 1; ch < NCH; ++ch) P = z48(P) ^ la[ch];
+      if (hl == 0) P ^= zseg(zt, carry);
+      // scan within the octet
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t dd = 1u << k;
+        const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)P);
+        if (hl >= dd) P = zseg_xor(zt + 1024 * k, prev, P);
+      }
+      uint32_t r[NCH];
+      {
+        const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)P);
+        r[0] = hl == 0 ? carry : pr;
+      }
+#pragma unroll
+      for (uint32_t ch = 1; ch < NCH; ++ch) r[ch] = z48(r[ch - 1]) ^ la[ch - 1];
+      // pass B: word checks; a valid hit at byte bi of the segment means base + bi + 1 in [m + 4, L]
+      const int64_t lo64 = m + 3 - base, hi64 = L - 1 - base;
+      const int32_t vlo = lo64 < 0 ? 0 : (lo64 > (int64_t)SEG ? (int32_t)SEG : (int32_t)lo64);
+      const int32_t vhi = hi64 < 0 ? -1 : (hi64 > (int64_t)SEG ? (int32_t)SEG : (int32_t)hi64);
+      const uint64_t actm = __builtin_amdgcn_ballot_w64(act);
+      uint32_t best = 0xFFu;  // the lane's smallest valid hit byte (0xFF: none)
+#pragma unroll
+      for (uint32_t i = 0; i < CW; ++i) {
+#pragma unroll
+        for (uint32_t ch = 0; ch < NCH; ++ch) {
+          const uint32_t j = CW * ch + i, w = u[j], rr = r[ch];
+          const bool h1 = (rr ^ (w & 0xFFu)) == kResBack1, h2 = (rr ^ (w & 0xFFFFu)) == kResBack2;
+          const bool h3 = (rr ^ (w & 0xFFFFFFu)) == kResBack3;
+          const uint32_t xx = rr ^ w;
+          const bool h4 = xx == kResBack4;
+          const uint64_t any = (__builtin_amdgcn_ballot_w64(h1) | __builtin_amdgcn_ballot_w64(h2) |
+                                __builtin_amdgcn_ballot_w64(h3) | __builtin_amdgcn_ballot_w64(h4)) & actm;
+          if (any) {
+            const bool hk[4] = {h1, h2, h3, h4};
+#pragma unroll
+            for (uint32_t kk = 0; kk < 4; ++kk) {
+              const int32_t bi = (int32_t)(4 * j + kk);
+              if (hk[kk] && bi >= vlo && bi <= vhi && (uint32_t)bi < best) best = (uint32_t)bi;
+            }
+          }
+          if (i + 1 < CW) r[ch] = ustep_xor(lds, xx, 0u, ub0, ub1);
+        }
+      }
+      const uint64_t hitm = __builtin_amdgcn_ballot_w64(best != 0xFFu) & actm;
+      if (hitm) {
+        const uint32_t om = (uint32_t)(hitm >> (LPC * oct)) & ((1u << LPC) - 1u);
+        const uint32_t fl = LPC * oct + (om ? (uint32_t)__builtin_ctz(om) : 0u);
+        const uint32_t fb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(fl * 4u), (int)best);
+        if (act && om) found = B + (int64_t)(SEG * (fl - LPC * oct) + fb) + 1 - 4;
+      }
+      carry = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane | (LPC - 1)) * 4u), (int)P);
+      act = act && found < 0 && B + (int64_t)(LPC * SEG) < L;
+    }
+    if (live && hl == 0) result[c] = found;
+  }
+}
+#endif  // LNX_RESEARCH
+
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
@@ -863,6 +1032,11 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
         else
           hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 2>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
                              bytes, off, min_off, n, tables, result);
+      } else if (mode == 'o') {  // octet segments: 8 lanes x 192 bytes per capture, 8 captures per wave
+        uint64_t g1 = ((n + 7) / 8 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
+        hipLaunchKernelGGL(crc32_search_o_kernel, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
+                           min_off, n, tables, result);
       } else if (mode == 'q') {  // U layout, two captures per half, each segment as two 24-byte chains
         uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
         if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;

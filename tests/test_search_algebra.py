@@ -127,6 +127,85 @@ def seg_search(data: bytes, min_off: int, SEG: int = 24, LANES: int = 64, KZ: in
     return -1
 
 
+def oct_search(data: bytes, min_off: int) -> int:
+    """crc32_search_o_kernel (research, LNX_PROF_SEARCH=o): 8 lanes x 192 bytes
+    per 1536-byte block; each lane folds four 48-byte chains from 0 (la_c),
+    joins them by Horner with Z_48, the 3-level scan uses Z_{192*2^k}, pass B
+    enters chain c + 1 at Z_48(r_c) ^ la_c and checks words; each lane keeps its
+    smallest valid hit byte and the first lane with a hit answers."""
+    SEG, LANES, CW = 192, 8, 12
+    if SEG not in _ZLEVELS:
+        _ZLEVELS[SEG] = [_zshift_table(SEG << k) for k in range(3)]
+    zl = _ZLEVELS[SEG]
+    z48 = _ZLEVELS.setdefault("z48", _zshift_table(48))
+    L = len(data)
+    m = max(min_off, 0)
+    if L < m + 4:
+        return -1
+    carry = 0xFFFFFFFF
+    for B in range(0, L, LANES * SEG):
+        words, la, l = [], [], []
+        for j in range(LANES):
+            seg = data[B + SEG * j: B + SEG * (j + 1)]
+            w = struct.unpack("<48I", seg + bytes(SEG - len(seg)))
+            words.append(w)
+            las = []
+            for ch in range(4):
+                x = w[CW * ch]
+                for i in range(CW - 1):
+                    x = _Z4(x) ^ w[CW * ch + i + 1]
+                las.append(_Z4(x))
+            p = las[0]
+            for ch in range(1, 4):
+                p = z48(p) ^ las[ch]
+            if j == 0:
+                p ^= zl[0](carry)
+            la.append(las)
+            l.append(p)
+        P = list(l)
+        for k in range(3):
+            d = 1 << k
+            P = [P[j] ^ (zl[k](P[j - d]) if j >= d else 0) for j in range(LANES)]
+        for j in range(LANES):
+            base = B + SEG * j
+            r = [carry if j == 0 else P[j - 1]]
+            for ch in range(1, 4):
+                r.append(z48(r[ch - 1]) ^ la[j][ch - 1])
+            best = None
+            for i in range(CW):
+                for ch in range(4):
+                    wi = CW * ch + i
+                    w = words[j][wi]
+                    for kk in range(1, 5):
+                        lo = 0xFFFFFFFF >> (32 - 8 * kk)
+                        bi = 4 * wi + kk - 1
+                        if r[ch] ^ (w & lo) == RESIDUE_BACK[kk] and m + 4 <= base + bi + 1 <= L:
+                            best = bi if best is None else min(best, bi)
+                    r[ch] = _Z4(r[ch] ^ w)
+            if best is not None:
+                return base + best + 1 - 4
+        carry = P[LANES - 1]
+    return -1
+
+
+def test_oct_schedule_matches_oracle():
+    rng = np.random.default_rng(37)
+    cases = []
+    for n in [0, 3, 4, 5, 47, 48, 49, 191, 192, 193, 1499, 1536, 1537, 3100]:
+        body = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        cases.append((body, 0))
+        cases.append((body + struct.pack("<I", O.crc32(body)), 0))
+        cases.append((body + struct.pack("<I", O.crc32(body)) + body[:40], n))
+        cases.append((body + struct.pack("<I", O.crc32(body)) + body[:40], n + 1))
+    cases.append((b"\0\0\0\0" + bytes(100), 0))
+    # hits straddling chains, lane segments and the block edge
+    for cut in [44, 45, 46, 47, 92, 140, 141, 188, 189, 190, 191, 380, 1532, 1533, 1534, 1535, 1536, 3068]:
+        body = rng.integers(0, 256, size=cut, dtype=np.uint8).tobytes()
+        cases.append((body + struct.pack("<I", O.crc32(body)) + bytes(9), 0))
+    for data, mo in cases:
+        assert oct_search(data, mo) == O.crc32_search(data, mo), (len(data), mo)
+
+
 def test_split_chain_identity():
     """crc32_search_u_kernel<NC, SPLIT>: a 48-byte segment folded as two
     24-byte chains joins as Z_24(la) ^ lb, and pass B's second chain starts from
