@@ -232,6 +232,107 @@ def rx_ring_bench(args, L, synth, torch, dev, world):
     print(json.dumps(out), flush=True)
 
 
+def _udp4_frames(synth, n, cap, lens):
+    """n UDP/IPv4 Ethernet frames of lens[i] bytes, frame i = rows[i, :lens[i]]
+    of a pageable (n, cap) array: random payload, headers the TX generate and
+    the receive verdicts accept (EtherType 0x0800, IHL 5, DF, TTL 64, UDP)."""
+    rows = synth.bytes_np(n * cap, seed=synth.SEED).reshape(n, cap)
+    rows[:, 0:6] = (0x02, 0x00, 0x00, 0x00, 0x00, 0x01)
+    rows[:, 6:12] = (0x02, 0x00, 0x00, 0x00, 0x00, 0x02)
+    rows[:, 12:16] = (0x08, 0x00, 0x45, 0x00)
+    ip_len = (lens - 14).astype(np.uint32)
+    rows[:, 16] = (ip_len >> 8) & 0xFF
+    rows[:, 17] = ip_len & 0xFF
+    rows[:, 20:24] = (0x40, 0x00, 64, 17)
+    rows[:, 24:26] = 0
+    rows[:, 26:34] = (10, 0, 0, 1, 10, 0, 0, 2)
+    udp_len = (lens - 34).astype(np.uint32)
+    rows[:, 38] = (udp_len >> 8) & 0xFF
+    rows[:, 39] = udp_len & 0xFF
+    rows[:, 40:42] = 0
+    return rows
+
+
+def packets_bench(args, L, synth, torch, dev, world):
+    """The netdev batch boundary end to end (x/netdev/interface.go:85-89,
+    DESIGN.md §4): per-frame pageable host buffers, as a Go stack hands them
+    over.  egress_packets: lnx_egress_packets with LNX_TX_CHECKSUM | LNX_TX_FCS
+    (gather into pinned staging, H2D, TX checksum generate + padding + FCS
+    append, D2H, scatter back into the buffers); ingress_packets:
+    lnx_ingress_packets (gather, H2D, FCS verify + receive verdicts, D2H).
+    1 M frames, --workload mtu1500 (1500 B on the wire) or zipf64_1500.
+    Host wall clock per step; never the headline `value`."""
+    if world != 1:
+        raise SystemExit(f"--op {args.op} runs on one GPU")
+    n, cap = 1 << 20, 1536
+    zipf = args.workload == "zipf64_1500"
+    wire = synth.zipf_lengths(n).astype(np.int64) if zipf else np.full(n, FRAME_BYTES, dtype=np.int64)
+    rows = _udp4_frames(synth, n, cap, wire)
+    ptrs = (rows.ctypes.data + cap * np.arange(n, dtype=np.uint64)).astype(np.uint64)
+    ring = L.RxRing(args.ring_batch, slot_cap=cap,  # (the packet calls stage through the ring; its slots stay unused)
+                    batch_slots=args.ring_batch, depth=args.ring_depth)
+    status = np.zeros(n, dtype=np.uint8)
+    verdict = np.zeros(n, dtype=np.uint8)
+    try:
+        if args.op == "egress_packets":
+            sizes0 = (wire - 4).astype(np.uint32)  # the stack's frame; the device adds the FCS
+            lens = sizes0.copy()
+
+            def step():
+                lens[:] = sizes0
+                rc = L.lib.lnx_egress_packets(ring._h, ptrs.ctypes.data, lens.ctypes.data, n, 0, cap,
+                                              L.TX_CHECKSUM | L.TX_FCS, status.ctypes.data)
+                if rc != 0:
+                    raise L.LnetoError(f"lnx_egress_packets: {rc}")
+            step()
+            assert (lens == wire.astype(np.uint32)).all() and (status == 0).all(), "egress: unexpected lengths/status"
+            room = np.maximum(sizes0.astype(np.int64), 60) + 4
+            h2d = int(room.sum()) + 12 * n
+            d2h = int(room.sum()) + 6 * n
+            what = "gather -> H2D -> TX checksum generate + pad + FCS append -> D2H -> scatter"
+        else:
+            # frames already finished by the transmit path: run egress once to give them checksums + FCS
+            sizes0 = (wire - 4).astype(np.uint32)
+            lens = sizes0.copy()
+            rc = L.lib.lnx_egress_packets(ring._h, ptrs.ctypes.data, lens.ctypes.data, n, 0, cap,
+                                          L.TX_CHECKSUM | L.TX_FCS, status.ctypes.data)
+            assert rc == 0 and (status == 0).all()
+            lens = wire.astype(np.uint32)
+
+            def step():
+                rc = L.lib.lnx_ingress_packets(ring._h, ptrs.ctypes.data, lens.ctypes.data, n, 0, 0,
+                                               status.ctypes.data, verdict.ctypes.data)
+                if rc != 0:
+                    raise L.LnetoError(f"lnx_ingress_packets: {rc}")
+            step()
+            assert (status == 1).all() and (verdict == 0).all(), "ingress: valid frames not accepted"
+            h2d = int(wire.sum()) + 8 * (n + -(-n // args.ring_batch))
+            d2h = 2 * n
+            what = "gather -> H2D -> FCS verify + receive verdicts -> D2H"
+        for _ in range(max(args.warmup, 1) - 1):
+            step()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        el = (time.perf_counter() - t0) / args.steps
+    finally:
+        ring.close()
+    nbytes = int(wire.sum())
+    out = {
+        "metric": f"GiB/s {args.op} (per-frame pageable buffers: {what})",
+        "value": round(nbytes / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic UDP/IPv4 {'Zipf 64-1500 B' if zipf else '1500-byte'} frames (on the wire), "
+                f"one pageable {cap}-byte buffer each",
+        "config": {"workload": f"1M {'Zipf-mix' if zipf else 'x 1500 B'} frames in host memory", "frames": n,
+                   "frame_bytes": nbytes, "pcie_h2d_bytes_per_step": h2d, "pcie_d2h_bytes_per_step": d2h,
+                   "mpps": round(n / el / 1e6, 2), "depth": args.ring_depth, "batch_slots": args.ring_batch,
+                   "kernel": L.version()},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def slice16m_bench(L, synth, torch, dev, steps: int = 10, warmup: int = 3):
     """configs[4]'s per-GPU slice (16 M x 1500 B, 24 GB) on this one GPU: the
     per-rank work of every N>1 run, so value_N / (N * slice16m) compares equal
@@ -266,7 +367,7 @@ def main():
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32",
                     choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search",
-                             "tx_checksum"])
+                             "tx_checksum", "egress_packets", "ingress_packets"])
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
@@ -313,6 +414,8 @@ def main():
 
     if args.op == "rx_ring":
         return rx_ring_bench(args, L, synth, torch, dev, world)
+    if args.op in ("egress_packets", "ingress_packets"):
+        return packets_bench(args, L, synth, torch, dev, world)
 
     wname, n_rank, flen, desc = workload_spec(args.workload, world)
     if cpu_ranks:
