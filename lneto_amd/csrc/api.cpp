@@ -24,7 +24,7 @@ uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
                               uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              const void* image, int num_cus, hipStream_t stream);
+                              int fold, const void* image, int num_cus, hipStream_t stream);
 #endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
@@ -122,11 +122,13 @@ std::vector<uint32_t> build_lanes_image() {
 // tables A[e] = Z_2(e), B[e] = Z_1(e), then Z_{2^m} as eight nibble tables
 // for m = 0..30, entry (m, i, v) at dword 512 + 128 m + 16 i + v.
 std::vector<uint32_t> build_stage_image() {
-  std::vector<uint32_t> t(512 + 31 * 128);
+  std::vector<uint32_t> t(512 + 31 * 128 + 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 2), t[256 + e] = zshift_bytes(e, 1);
   for (uint32_t m = 0; m < 31; ++m)
     for (uint32_t i = 0; i < 8; ++i)
       for (uint32_t v = 0; v < 16; ++v) t[512 + 128 * m + 16 * i + v] = zshift_bytes_fast(v << (4 * i), 1ull << m);
+  for (uint32_t k = 0; k < 4; ++k)  // Z_4 byte tables (the FOLD 4 variants)
+    for (uint32_t e = 0; e < 256; ++e) t[512 + 31 * 128 + 256 * k + e] = zshift_bytes(e << (8 * k), 4);
   return t;
 }
 
@@ -538,10 +540,11 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  // 300 / 301: the staged lane streams (stage_kernel.hip), CRC / FCS verify
-  hipError_t e = var == 300 || var == 301
-                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var == 301, c->d_stage, c->num_cus,
-                                          static_cast<hipStream_t>(stream))
+  // 300 / 301: the staged lane streams (stage_kernel.hip), CRC / FCS verify,
+  // slicing-by-2 fold; 302 / 303: the same with the 16-column Z_4 fold
+  hipError_t e = var >= 300 && var <= 303
+                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1, var >= 302 ? 4 : 2, c->d_stage,
+                                          c->num_cus, static_cast<hipStream_t>(stream))
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                             static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");

@@ -57,7 +57,9 @@ constexpr uint32_t kSCtr = kSNib + 31 * 512;                // the workgroup's b
 constexpr uint32_t kStageLdsBytes = kSCtr + 16;
 static_assert(kStageLdsBytes <= 163840, "stage LDS");
 // compact image in HBM (api.cpp build_stage_image): A[256], B[256], then the
-// nibble tables verbatim (512 + 31 * 128 dwords)
+// nibble tables verbatim (512 + 31 * 128 dwords), then (FOLD 4) the four Z_4
+// byte tables, table k entry e at kStageZ4Img + 256 k + e
+constexpr uint32_t kStageZ4Img = 512 + 31 * 128;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -70,8 +72,27 @@ __device__ __forceinline__ uint32_t s_z2(const char* lds, uint32_t v, uint32_t b
   const uint32_t a = __builtin_amdgcn_perm(v, b0, 0x0c020400u), b = __builtin_amdgcn_perm(v, b0, 0x0c020500u);
   return __builtin_amdgcn_bitop3_b32(v >> 16, s_lds(lds, kSTab + a), s_lds(lds, kSTab + b + 128u), 0x96);
 }
+// FOLD 2: Z_1 is table B.  FOLD 4 (variants 302 / 303): the four Z_4 byte
+// tables in 16 bank columns, entry e of table k, column c at e << 8 | k << 6 |
+// c << 2 (64 KiB like FOLD 2's; lanes c and c + 16 share a column, so every
+// lookup is a 2-way bank conflict), one LDS round trip per dword instead of
+// two; Z_1 is its table 3 (Z_4(e << 24) = Z_1(e)).
+template <int FOLD>
 __device__ __forceinline__ uint32_t s_z1(const char* lds, uint32_t v, uint32_t b0) {
-  return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + 128u);
+  return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + (FOLD == 4 ? 192u : 128u));
+}
+// Z_4(v)
+template <int FOLD>
+__device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b0) {
+  if constexpr (FOLD == 4) {
+    const uint32_t a0 = __builtin_amdgcn_perm(v, b0, 0x0c020400u), a1 = __builtin_amdgcn_perm(v, b0, 0x0c020500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(v, b0, 0x0c020600u), a3 = __builtin_amdgcn_perm(v, b0, 0x0c020700u);
+    return __builtin_amdgcn_bitop3_b32(s_lds(lds, kSTab + a0), s_lds(lds, kSTab + a1 + 64u),
+                                       s_lds(lds, kSTab + a2 + 128u), 0x96) ^
+           s_lds(lds, kSTab + a3 + 192u);
+  } else {
+    return s_z2(lds, s_z2(lds, v, b0), b0);
+  }
 }
 // Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
 // nibble value picks one of 16 banks, equal values broadcast)
@@ -102,20 +123,31 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE>
+template <StageMode MODE, int FOLD>
 __global__ void __launch_bounds__(kStageThreads, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char lds[kStageLdsBytes];
   // ---- image: A / B values expanded into their 32 bank columns, nibble tables verbatim
   {
-    const uint32_t t = threadIdx.x;  // 512 threads: one A or B value each
-    const uint32_t v = image[t];
-    const uint32_t m = t >> 8, e = t & 255u;
-    uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
-    const uint4 v4 = {v, v, v, v};
+    const uint32_t t = threadIdx.x;  // 512 threads: one A or B value each (FOLD 4: two Z_4 values)
+    if constexpr (FOLD == 4) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+      for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t vi = t + 512u * h, v = image[kStageZ4Img + vi];
+        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 6));
+        const uint4 v4 = {v, v, v, v};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[(i + t) & 3u] = v4;
+      }
+    } else {
+      const uint32_t v = image[t];
+      const uint32_t m = t >> 8, e = t & 255u;
+      uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
+      const uint4 v4 = {v, v, v, v};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+    }
     for (uint32_t i = t; i < 31u * 128u; i += kStageThreads)
       reinterpret_cast<uint32_t*>(lds + kSNib)[i] = image[512 + i];
     if (t == 0) *reinterpret_cast<uint32_t*>(lds + kSCtr) = 0;
@@ -126,7 +158,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint64_t fb1 = fb0 + frames_per_wg < nframes ? fb0 + frames_per_wg : nframes;
   const uint32_t nslice = (uint32_t)(fb1 - fb0);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t b0 = (lane & 31u) << 2;
+  const uint32_t b0 = (lane & (FOLD == 4 ? 15u : 31u)) << 2;
   char* tr = lds + kSTr + 8192u * wv;
   uint32_t* list = reinterpret_cast<uint32_t*>(lds + kSBnd + 1536u * wv);
   constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
@@ -171,7 +203,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           const bool act = q < e;
           if (__builtin_amdgcn_ballot_w64(act) == 0) break;
           const uint32_t b = bytes[act ? q : A];
-          const uint32_t nr = s_z1(lds, r ^ b, b0);
+          const uint32_t nr = s_z1<FOLD>(lds, r ^ b, b0);
           r = act ? nr : r;
         }
         if (j < bf) {
@@ -326,7 +358,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
               r = ev ? 0xFFFFFFFFu : r;
               advance(ev);
             }
-            r = s_z1(lds, r ^ (w >> (8u * (b & 3u))), b0);
+            r = s_z1<FOLD>(lds, r ^ (w >> (8u * (b & 3u))), b0);
           }
           continue;
         }
@@ -341,13 +373,13 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
           const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
           const uint32_t v = at ? vr : r ^ w;
-          r = s_z2(lds, s_z2(lds, v, b0), b0);
+          r = s_z4<FOLD>(lds, v, b0);
         }
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
           uint32_t S = ecap;  // Z_c(e), c = 0..3
 #pragma unroll
           for (uint32_t s = 0; s < 3; ++s) {
-            const uint32_t z = s_z1(lds, S, b0);
+            const uint32_t z = s_z1<FOLD>(lds, S, b0);
             S = s < c ? z : S;
           }
           end_at(in, S, x, (int)h);
@@ -405,18 +437,21 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              const void* image, int num_cus, hipStream_t stream) {
+                              int fold, const void* image, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   uint64_t grid = (n + kStageBF - 1) / kStageBF;
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const uint64_t per = (n + grid - 1) / grid;
   const uint32_t* img = static_cast<const uint32_t*>(image);
-  if (verify)
-    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3((unsigned)grid), dim3(kStageThreads), 0, stream,
-                       bytes, off, n, per, img, out);
-  else
-    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3((unsigned)grid), dim3(kStageThreads), 0, stream,
-                       bytes, off, n, per, img, out);
+#define LNX_STAGE(M, F)                                                                                      \
+  hipLaunchKernelGGL((crc32_stage_kernel<M, F>), dim3((unsigned)grid), dim3(kStageThreads), 0, stream, bytes, off, \
+                     n, per, img, out)
+  if (fold == 4) {
+    if (verify) LNX_STAGE(StageMode::kVerify, 4); else LNX_STAGE(StageMode::kCrc, 4);
+  } else {
+    if (verify) LNX_STAGE(StageMode::kVerify, 2); else LNX_STAGE(StageMode::kCrc, 2);
+  }
+#undef LNX_STAGE
   return hipGetLastError();
 }
 

@@ -1,15 +1,18 @@
 """Staged lane streams (lneto_amd/csrc/stage_kernel.hip) on the
 GPU against the C oracle (Go hash/crc32 IEEE restated; the arithmetic of
 ethernet.CRC32, lneto ethernet/crc.go:19-21): the Zipf mix, every length
-0..700 at odd lead-ins, tiny and empty frames (the byte-serial halves),
+0..700 at odd lead-ins (variants 300 / 302: the two folds), tiny and empty frames (the byte-serial halves),
 frames longer than a stretch (the carry chain), jumbo and gigantic frames,
-tiny batches, and FCS verify (variant 301) with one flipped byte per frame
+tiny batches, and FCS verify (variants 301 / 303) with one flipped byte per frame
 for a third of the frames.  The schedule's algebra is pinned on the host in
 tests/test_stage_algebra.py."""
 import ctypes
 
 import numpy as np
 import pytest
+
+
+CRC_VARS = [300, 302]  # slicing-by-2 fold / 16-column Z_4 fold
 
 
 def _lib():
@@ -30,76 +33,82 @@ def _run(cuda, data, off, var=300):
     assert rc == 0
     torch.cuda.synchronize()
     got = out.cpu().numpy().view(np.uint32)[:n]
-    return got if var == 300 else got.view(np.uint8)[:n]
+    return got if var % 2 == 0 else got.view(np.uint8)[:n]
 
 
-def _check(cuda, off, seed, name):
+def _check(cuda, off, seed, name, var=300):
     from lneto_amd import synth
     from oracle import oracle as O
     off = np.asarray(off, dtype=np.uint64)
     data = synth.bytes_np(int(off[-1]) + 8, seed=seed)
-    got = _run(cuda, data, off)
+    got = _run(cuda, data, off, var)
     want = O.crc32_frames(data, off, threads=8)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{name}: wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]}) of {len(off) - 1}"
 
 
 @pytest.mark.gpu
-def test_gpu_stage_zipf(cuda):
+@pytest.mark.parametrize("var", CRC_VARS)
+def test_gpu_stage_zipf(cuda, var):
     from lneto_amd import synth
     for n, seed in ((1 << 16, 11), (1 << 20, 12), (300_001, 13)):
-        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}")
+        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stage_all_lengths(cuda):
+@pytest.mark.parametrize("var", CRC_VARS)
+def test_gpu_stage_all_lengths(cuda, var):
     from lneto_amd import synth
     rng = np.random.default_rng(9)
     for lead in (0, 1, 2, 3, 5, 64, 127):
         lens = rng.permutation(np.arange(0, 701))
         off = np.concatenate([[0], synth.offsets_from_lengths(lens) + lead])
-        _check(cuda, off, 100 + lead, f"lengths lead {lead}")
+        _check(cuda, off, 100 + lead, f"lengths lead {lead}", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stage_tiny_and_empty(cuda):
+@pytest.mark.parametrize("var", CRC_VARS)
+def test_gpu_stage_tiny_and_empty(cuda, var):
     """Several boundaries in one 64-byte half: the byte-serial path."""
     from lneto_amd import synth
     rng = np.random.default_rng(21)
     for trial in range(4):
         lens = rng.choice([0, 0, 1, 2, 3, 4, 5, 7, 9, 15, 16, 17, 33, 64, 200], size=20000 + 977 * trial)
         off = np.concatenate([[0], synth.offsets_from_lengths(lens) + trial * 37])
-        _check(cuda, off, 200 + trial, f"tiny {trial}")
+        _check(cuda, off, 200 + trial, f"tiny {trial}", var)
     lens = np.concatenate([np.full(50000, 64), synth.zipf_lengths(50000, seed=5), np.full(3000, 1)])
-    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed")
+    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stage_long_frames(cuda):
+@pytest.mark.parametrize("var", CRC_VARS)
+def test_gpu_stage_long_frames(cuda, var):
     """Frames longer than a stretch (the carry runs through stretches without
     a boundary), jumbo frames, a 3 MiB frame among short ones."""
     from lneto_amd import synth
     rng = np.random.default_rng(31)
     lens = rng.choice([9000, 1500, 64, 0, 100_000], size=3000)
-    _check(cuda, synth.offsets_from_lengths(lens), 400, "long")
+    _check(cuda, synth.offsets_from_lengths(lens), 400, "long", var)
     lens = np.array([60] * 500 + [3 << 20] + [60] * 500 + [1500] * 2000)
-    _check(cuda, synth.offsets_from_lengths(lens), 401, "3 MiB")
-    _check(cuda, synth.offsets_from_lengths(np.full(20000, 9000)), 402, "jumbo")
-    _check(cuda, synth.offsets_from_lengths(np.full(100000, 1500)), 403, "mtu")
+    _check(cuda, synth.offsets_from_lengths(lens), 401, "3 MiB", var)
+    _check(cuda, synth.offsets_from_lengths(np.full(20000, 9000)), 402, "jumbo", var)
+    _check(cuda, synth.offsets_from_lengths(np.full(100000, 1500)), 403, "mtu", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stage_small_batches(cuda):
+@pytest.mark.parametrize("var", CRC_VARS)
+def test_gpu_stage_small_batches(cuda, var):
     from lneto_amd import synth
     rng = np.random.default_rng(41)
     for n in (1, 2, 3, 63, 64, 65, 381, 382, 383, 765, 1000):
         lens = rng.integers(0, 400, size=n)
         for lead in (0, 13, 127):
-            _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(lens) + lead]), n + lead, f"n {n} lead {lead}")
+            _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(lens) + lead]), n + lead, f"n {n} lead {lead}", var)
 
 
 @pytest.mark.gpu
-def test_gpu_stage_verify(cuda):
+@pytest.mark.parametrize("var", [301, 303])
+def test_gpu_stage_verify(cuda, var):
     """Variant 301: FCS verify (residue) over frames carrying their LE FCS;
     a third get one flipped byte; runts under 4 bytes fail."""
     from lneto_amd import synth
@@ -118,7 +127,7 @@ def test_gpu_stage_verify(cuda):
         s, e = int(off[i]), int(off[i + 1])
         if e > s:
             data[s + int(rng.integers(0, e - s))] ^= 0x40
-    got = _run(cuda, data, off, var=301)
+    got = _run(cuda, data, off, var=var)
     want = np.array([int(int(off[i + 1]) - int(off[i]) >= 4 and O.c_crc32(data[int(off[i]):int(off[i + 1])].tobytes())
                          == 0x2144DF1C) for i in range(len(lens))], dtype=np.uint8)
     bad = np.nonzero(got != want)[0]
