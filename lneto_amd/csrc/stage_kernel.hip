@@ -221,8 +221,12 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     uint32_t Q = ((sp + 63u) / 64u + 127u) & ~127u;
     Q = Q < 128u ? 128u : Q;
     const uint32_t rounds = Q / 128u;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pa - adj), (short)0, (int)sp, 0x00020000);
+    // the range rounded up to whole 16-byte pieces: a load that straddles the
+    // range end reads as 0, and the block's last frame ends in it (the bytes
+    // past E only feed states past the last boundary; the base is 128-aligned,
+    // so the piece holding E's last byte never crosses a page)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pa - adj), (short)0,
+                                                                        (int)((sp + 15u) & ~15u), 0x00020000);
     // ---- this lane's stretch [Sk, Sk + Q) and its first boundary j = lower_bound(list, Sk)
     const uint32_t Sk = lane * Q;
     uint32_t lo = 0, hi = bf + 1u;
