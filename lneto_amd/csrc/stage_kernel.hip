@@ -239,7 +239,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     }
     const uint32_t jstart = lo;
     uint32_t j = lo;
-    uint32_t x = list[j], x1 = list[j + 1u];
+    uint32_t x = list[j], x1 = list[j + 1u < 383u ? j + 1u : 383u];  // (j = bf + 1 past the block end)
     uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
     uint32_t r = 0;
     bool first = true;
