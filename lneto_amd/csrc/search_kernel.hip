@@ -768,7 +768,6 @@ constexpr uint32_t kOctNibOff = kZ24Off + 1024;          // host tables: Z_48 ni
 constexpr uint32_t kOctLdsDwords = 32768 + 4096 + 3 * 1024;
 static_assert(kOctLdsDwords * 4 <= 163840, "octet LDS");
 
-#ifdef LNX_RESEARCH
 __global__ void __launch_bounds__(kSegBlock, 1)
 crc32_search_o_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                       const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
@@ -914,20 +913,19 @@ crc32_search_o_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
     if (live && hl == 0) result[c] = found;
   }
 }
-#endif  // LNX_RESEARCH
 
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-#ifndef LNX_RESEARCH
-  // product: word checks, every Z_4 step through the lane-private U layout, one
-  // block per CU, two captures per half-wave (r2s2f)
-  {
-    uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+  auto launch_octets = [&]() {
+    uint64_t g1 = ((n + 7) / 8 + kSegBlock / 64 - 1) / (kSegBlock / 64);
     if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-    hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off, min_off,
-                       n, tables, result);
-  }
+    hipLaunchKernelGGL(crc32_search_o_kernel, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off, min_off, n,
+                       tables, result);
+  };
+#ifndef LNX_RESEARCH
+  // product: octet segments, 8 captures per wave (r4)
+  launch_octets();
 #else
   // research library:
   // LNX_PROF_SEARCH=word selects the word-lane kernel
@@ -1032,22 +1030,18 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
         else
           hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 2>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
                              bytes, off, min_off, n, tables, result);
-      } else if (mode == 'o') {  // octet segments: 8 lanes x 192 bytes per capture, 8 captures per wave
-        uint64_t g1 = ((n + 7) / 8 + kSegBlock / 64 - 1) / (kSegBlock / 64);
+      } else if (mode == 'U') {  // the r2 / r3 product: four captures per wave, 48-byte segments
+        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
         if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-        hipLaunchKernelGGL(crc32_search_o_kernel, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
+        hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
                            min_off, n, tables, result);
       } else if (mode == 'q') {  // U layout, two captures per half, each segment as two 24-byte chains
         uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
         if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
         hipLaunchKernelGGL((crc32_search_u_kernel<2, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
                            off, min_off, n, tables, result);
-      } else {  // product: word checks, every Z_4 step through the lane-private U layout, one block per CU,
-                // two captures per half-wave (r2s2f; prefetching the next group's words measured slower, r2s2g)
-        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
-        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-        hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
-                           min_off, n, tables, result);
+      } else {  // the product (octet segments)
+        launch_octets();
       }
     }
   }

@@ -410,7 +410,11 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     const bool hb = j > jstart;  // this stretch holds a boundary
     const uint32_t up = ((lane + 63u) & 63u) << 2;
     const uint32_t Ep = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)E1);
-    const bool hbp = lane == 0 || __builtin_amdgcn_ds_bpermute((int)up, (int)hb) != 0;
+    // (evaluated by every lane: under `lane == 0 || ...` hipcc runs the
+    // bpermute with lane 0 masked off, and a read from an inactive lane
+    // returns 0, so lane 1 saw "no boundary" in lane 0)
+    const int hbv = __builtin_amdgcn_ds_bpermute((int)up, (int)hb);
+    const bool hbp = (lane == 0) | (hbv != 0);
     uint32_t Pk = Ep;
     if (__builtin_amdgcn_ballot_w64(rec && !hbp) != 0) {
       // a frame longer than a stretch: P_k = Z_Q(P_{k-1}) ^ E_{k-1} through

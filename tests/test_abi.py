@@ -110,7 +110,7 @@ def test_product_library_holds_only_product_kernels():
         assert re.search(r"CrcModeE\dELi0E", k), k          # VAR = 0
         assert re.search(r"ELi0EEEvPKh", k), k              # STR = 0
     others = sorted(re.sub(r"^_ZN3lnx\d+(\w+?kernel).*$", r"\1", k) for k in ks if k not in rows)
-    assert others == ["crc32_search_u_kernel", "ingress_verify_kernel", "ingress_verify_kernel",
+    assert others == ["crc32_search_o_kernel", "ingress_verify_kernel", "ingress_verify_kernel",
                       "ring_segments_kernel", "sum16_lines_kernel"], others
     research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
     if os.path.exists(research):

@@ -28,7 +28,14 @@ s_mov_b64 exec restore it; the body of a loop whose latch retires lanes counts
 as narrowed) and flags a cross-lane read whose source has no write, anywhere
 before it in the kernel, at an exec depth no narrower than the read's own.
 
-usage: audit_loops.py file.s [symbol-regex]   (exit 1 if any loop or read is flagged)
+Third check (round 4, --masked, report only): a cross-lane read issued while
+exec is narrowed (`masked_cross_lane_reads`): its reads of inactive lanes
+return 0.  The stage kernel's first carry read lane 0 from under
+`lane == 0 || bpermute(...)`, which hipcc compiles with lane 0 masked off.
+The linear depth scan cannot follow every if / else join, so this list has
+false positives and does not set the exit status.
+
+usage: audit_loops.py file.s [symbol-regex] [--masked]   (exit 1 if any loop or stale read is flagged)
 """
 import re
 import sys
@@ -111,7 +118,13 @@ def exec_depths(body):
     for l in body:
         m = re.match(r"^(s_and_saveexec_b64|s_andn2_saveexec_b64|s_or_saveexec_b64)\s+(s\[\d+:\d+\])", l)
         r = re.match(r"^(s_or_b64 exec, exec,|s_mov_b64 exec,)\s*(s\[\d+:\d+\])", l)
-        if m and m.group(1) != "s_or_saveexec_b64":
+        e = re.match(r"^s_or_saveexec_b64\s+(s\[\d+:\d+\]),\s*(s\[\d+:\d+\])", l)
+        if e:
+            # the else arm of an if / else: the then-arm's saved mask becomes
+            # the else-arm's, closed later by s_or_b64 exec, exec, <new>
+            if e.group(2) in stack:
+                stack[stack.index(e.group(2))] = e.group(1)
+        elif m and m.group(1) != "s_or_saveexec_b64":
             stack.append(m.group(2))
         elif r and r.group(2) in stack:
             while stack and stack.pop() != r.group(2):
@@ -127,7 +140,10 @@ def exec_depths(body):
         m = re.match(r"^s_c?branch\w*\s+(\.LBB\w+)", l)
         if m and m.group(1) in labels and labels[m.group(1)] <= i:
             start = labels[m.group(1)]
-            if any(re.match(r"^s_andn2_b64 exec, exec,", t) for t in body[start:i + 1]):
+            # the latch block (from the last label before the backward branch)
+            # retires lanes: its own s_andn2_b64 exec, not a nested loop's
+            k0 = next(k for k in range(i, start - 1, -1) if re.match(r"^\.LBB\w+:", body[k]))
+            if any(re.match(r"^s_andn2_b64 exec, exec,", t) for t in body[k0:i + 1]):
                 for k in range(start, i + 1):
                     out[k] += 1
     return out
@@ -200,9 +216,28 @@ def stale_cross_lane_reads(body):
     return found
 
 
+MASKED = re.compile(r"(quad_perm:|row_shl:|row_shr:|row_ror:|row_mirror|row_half_mirror|row_bcast|wave_shl|wave_rol|"
+                    r"wave_shr|wave_ror|row_newbcast|row_share|row_xmask)|^(ds_swizzle_b32|ds_bpermute_b32|"
+                    r"v_permlane16_swap|v_permlane32_swap)")
+
+
+def masked_cross_lane_reads(body):
+    """[(line, instruction)] of cross-lane reads issued under a narrowed exec
+    (round 4, the stage kernel's first carry): a lane that reads an INACTIVE
+    lane through ds_bpermute / ds_swizzle gets 0, through DPP 0 or its own old
+    value, not the source lane's register.  hipcc narrows exec around a
+    cross-lane builtin that sits in the right operand of `||` / `&&` or in a
+    divergent branch; such a read is correct only if no active lane reads an
+    inactive one, which the ISA alone cannot show, so every one is listed."""
+    dep = exec_depths(body)
+    return [(i, l) for i, l in enumerate(body) if dep[i] > 0 and MASKED.search(l)]
+
+
 def main():
-    path = sys.argv[1]
-    pat = re.compile(sys.argv[2]) if len(sys.argv) > 2 else None
+    masked = "--masked" in sys.argv
+    args = [a for a in sys.argv[1:] if a != "--masked"]
+    path = args[0]
+    pat = re.compile(args[1]) if len(args) > 1 else None
     lines = [l.split(";")[0].strip() for l in open(path).read().split("\n")]
     bad = nread = 0
     for sym, a, b in kernels(lines):
@@ -216,6 +251,9 @@ def main():
         for i, l, r in stale_cross_lane_reads(body):
             print(f"{sym}: cross-lane read of v{r} with no earlier write at its exec depth: {l}")
             bad += 1
+        if masked:  # report only: the linear exec-depth scan over-counts across if / else joins
+            for i, l in masked_cross_lane_reads(body):
+                print(f"{sym}: cross-lane read under a narrowed exec (inactive source lanes read as 0): {l}")
     print(f"audit: {nread} cross-lane reads checked, {bad} findings", file=sys.stderr)
     sys.exit(1 if bad else 0)
 
