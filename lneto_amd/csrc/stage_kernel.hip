@@ -218,7 +218,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       continue;
     }
     const uint32_t sp = (uint32_t)span;
-    uint32_t Q = ((sp + 63u) / 64u + 127u) & ~127u;
+    // 64 Q > sp: the block's last boundary (at sp) must lie inside a stretch
+    uint32_t Q = ((sp + 64u) / 64u + 127u) & ~127u;
     Q = Q < 128u ? 128u : Q;
     const uint32_t rounds = Q / 128u;
     // the range rounded up to whole 16-byte pieces: a load that straddles the

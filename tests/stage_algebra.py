@@ -95,7 +95,7 @@ def stage_block(data: bytes, off, f0: int, bf: int, q: int, force_slow: bool = F
     out = {} if out is None else out
     a, e = off[f0], off[f0 + bf]
     a_al = a - (a % LINE)
-    assert q % LINE == 0 and 64 * q >= e - a_al
+    assert q % LINE == 0 and 64 * q > e - a_al
     bnd = [off[f0 + j] - a_al for j in range(bf + 1)] + [MASK]  # relative, sentinel
     nbytes = len(data)
 
@@ -175,7 +175,7 @@ def stage_crcs(data: bytes, off, bf: int = 512, force_slow: bool = False):
         a, e = off[f0], off[f0 + b]
         span = e - (a - a % LINE)
         q = max(LINE, -(-span // 64 // LINE) * LINE) if span else LINE
-        while 64 * q < span:
+        while 64 * q <= span:  # the last boundary (at span) must lie inside a stretch
             q += LINE
         stage_block(data, off, f0, b, q, force_slow, out)
     return [out[i] for i in range(n)]

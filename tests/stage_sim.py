@@ -17,7 +17,7 @@ def stage_block_sim(data: bytes, off, f0: int, bf: int, base_mod128: int = 0, ou
     adj = (base_mod128 + A) & 127
     span = E - A + adj if E > A else adj
     sp = span
-    Q = ((sp + 63) // 64 + 127) & ~127
+    Q = ((sp + 64) // 64 + 127) & ~127  # 64 Q > sp
     Q = max(Q, 128)
     rounds = Q // 128
     rng_end = (sp + 15) & ~15  # the descriptor's range

@@ -43,3 +43,29 @@ def test_reset_constants():
     """K_c = Z_{-c}(~0): c zero bytes forward give the CRC init back."""
     for c in range(4):
         assert S.zc(c, S.K[c]) == 0xFFFFFFFF
+
+
+def test_block_ending_on_a_stretch_multiple():
+    """A block whose span is exactly 64 Q under `64 Q >= span` left its last
+    boundary outside every stretch (the 1 M Zipf GPU run lost one frame that
+    way): Q is now the smallest line multiple with 64 Q > span."""
+    from tests import stage_sim as SIM
+    for lens, lead in (([128] * 64, 0), ([100] * 80 + [192], 0), ([64] * 127 + [64 + 127], 1)):
+        data, off = _case(5, lens, lead)
+        want = S.zlib_crcs(data, off)
+        assert S.stage_crcs(data, off, bf=len(lens)) == want
+        got = SIM.stage_block_sim(data, off, 0, len(lens), 0)
+        assert [got.get(i) for i in range(len(lens))] == want
+
+
+@pytest.mark.parametrize("kind", ["zipf", "tiny", "long"])
+def test_wave_simulation_matches_zlib(kind):
+    """tests/stage_sim.py follows the kernel's control flow (wave-uniform slow
+    halves, held results, carries) and must give every frame of the block."""
+    from tests import stage_sim as SIM
+    rng = random.Random(len(kind))
+    lens = _lens(kind, rng)[:120]
+    data, off = _case(11, lens, 37)
+    want = S.zlib_crcs(data, off)
+    got = SIM.stage_block_sim(data, off, 0, len(lens), 0)
+    assert [got.get(i) for i in range(len(lens))] == want
