@@ -363,7 +363,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
               r = ev ? 0xFFFFFFFFu : r;
               advance(ev);
             }
-            r = s_z1<FOLD>(lds, r ^ (w >> (8u * (b & 3u))), b0);
+            r = s_z1<FOLD>(lds, r ^ ((w >> (8u * (b & 3u))) & 0xFFu), b0);  // (one byte: Z_1 shifts r, not w)
           }
           continue;
         }
