@@ -24,7 +24,7 @@ uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
                               uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, const void* image, int num_cus, hipStream_t stream);
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
 #endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
@@ -541,10 +541,11 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   // 300 / 301: the staged lane streams (stage_kernel.hip), CRC / FCS verify,
-  // slicing-by-2 fold; 302 / 303: the same with the 16-column Z_4 fold
-  hipError_t e = var >= 300 && var <= 303
-                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1, var >= 302 ? 4 : 2, c->d_stage,
-                                          c->num_cus, static_cast<hipStream_t>(stream))
+  // slicing-by-2 fold; 302 / 303: the same with the 16-column Z_4 fold;
+  // 304-307: 300-303 with 10 waves per workgroup instead of 8
+  hipError_t e = var >= 300 && var <= 307
+                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1, (var & 2) ? 4 : 2, var >= 304 ? 10 : 8,
+                                          c->d_stage, c->num_cus, static_cast<hipStream_t>(stream))
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                             static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");

@@ -45,17 +45,22 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum class StageMode : int { kCrc = 0, kVerify = 1 };
 
-constexpr int kStageWaves = 8;
-constexpr int kStageThreads = kStageWaves * 64;
 constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
-// LDS layout (bytes)
-constexpr uint32_t kSTab = 0;                               // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
-constexpr uint32_t kSTr = 65536;                            // transposes: 8 KiB per wave
-constexpr uint32_t kSBnd = kSTr + kStageWaves * 8192;       // boundary lists: 1536 B per wave
-constexpr uint32_t kSNib = kSBnd + kStageWaves * 1536;      // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
-constexpr uint32_t kSCtr = kSNib + 31 * 512;                // the workgroup's block counter
-constexpr uint32_t kStageLdsBytes = kSCtr + 16;
-static_assert(kStageLdsBytes <= 163840, "stage LDS");
+// LDS layout (bytes) for W waves per workgroup.  W = 8: the Z_{2^m} nibble
+// tables live in LDS too; W = 10 (variants 304-307): they are read from the
+// image in HBM (only the carries use them, once per stretch), which frees the
+// room for two more waves' transposes and lists.
+constexpr uint32_t kSTab = 0;  // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
+template <int W>
+struct StageLds {
+  static constexpr uint32_t kTr = 65536;               // transposes: 8 KiB per wave
+  static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists: 1536 B per wave
+  static constexpr bool kNibInLds = W <= 8;
+  static constexpr uint32_t kNib = kBnd + W * 1536;    // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
+  static constexpr uint32_t kCtr = kNib + (kNibInLds ? 31 * 512 : 0);  // the workgroup's block counter
+  static constexpr uint32_t kBytes = kCtr + 16;
+  static_assert(kBytes <= 163840, "stage LDS");
+};
 // compact image in HBM (api.cpp build_stage_image): A[256], B[256], then the
 // nibble tables verbatim (512 + 31 * 128 dwords), then (FOLD 4) the four Z_4
 // byte tables, table k entry e at kStageZ4Img + 256 k + e
@@ -95,18 +100,27 @@ __device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b
   }
 }
 // Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
-// nibble value picks one of 16 banks, equal values broadcast)
-__device__ __forceinline__ uint32_t s_zpow2(const char* lds, uint32_t m, uint32_t v) {
-  const uint32_t t = kSNib + 512u * m;
+// nibble value picks one of 16 banks, equal values broadcast), from LDS or,
+// for W > 8, from the image in HBM (dword (m, i, v) at 512 + 128 m + 16 i + v)
+template <int W>
+__device__ __forceinline__ uint32_t s_zpow2(const char* lds, const uint32_t* image, uint32_t m, uint32_t v) {
   uint32_t a = 0;
+  if constexpr (StageLds<W>::kNibInLds) {
+    const uint32_t t = StageLds<W>::kNib + 512u * m;
 #pragma unroll
-  for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
+    for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
+  } else {
+    const uint32_t* t = image + 512u + 128u * m;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) a ^= t[16u * i + __builtin_amdgcn_ubfe(v, 4 * i, 4)];
+  }
   return a;
 }
 // Z_d(v), d < 2^31, by binary powers; lanes whose d is done keep their value
-__device__ __forceinline__ uint32_t s_zd(const char* lds, uint32_t d, uint32_t v) {
+template <int W>
+__device__ __forceinline__ uint32_t s_zd(const char* lds, const uint32_t* image, uint32_t d, uint32_t v) {
   for (uint32_t m = 0; __builtin_amdgcn_ballot_w64((d >> m) != 0u) != 0; ++m) {
-    const uint32_t z = s_zpow2(lds, m, v);
+    const uint32_t z = s_zpow2<W>(lds, image, m, v);
     v = ((d >> m) & 1u) ? z : v;
   }
   return v;
@@ -123,34 +137,39 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE, int FOLD>
-__global__ void __launch_bounds__(kStageThreads, 1)
+template <StageMode MODE, int FOLD, int W>
+__global__ void __launch_bounds__(W * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) char lds[kStageLdsBytes];
-  // ---- image: A / B values expanded into their 32 bank columns, nibble tables verbatim
+  using LY = StageLds<W>;
+  constexpr uint32_t kThreads = W * 64;
+  __shared__ __attribute__((aligned(16))) char lds[LY::kBytes];
+  // ---- image: A / B values expanded into their 32 bank columns (FOLD 4: the
+  // Z_4 values into 16), nibble tables verbatim
   {
-    const uint32_t t = threadIdx.x;  // 512 threads: one A or B value each (FOLD 4: two Z_4 values)
+    const uint32_t t = threadIdx.x;
     if constexpr (FOLD == 4) {
-#pragma unroll
-      for (uint32_t h = 0; h < 2; ++h) {
-        const uint32_t vi = t + 512u * h, v = image[kStageZ4Img + vi];
+      for (uint32_t vi = t; vi < 1024u; vi += kThreads) {
+        const uint32_t v = image[kStageZ4Img + vi];
         uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 6));
         const uint4 v4 = {v, v, v, v};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) row[(i + t) & 3u] = v4;
+        for (int i = 0; i < 4; ++i) row[(i + vi) & 3u] = v4;
       }
     } else {
-      const uint32_t v = image[t];
-      const uint32_t m = t >> 8, e = t & 255u;
-      uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
-      const uint4 v4 = {v, v, v, v};
+      for (uint32_t vi = t; vi < 512u; vi += kThreads) {
+        const uint32_t v = image[vi];
+        const uint32_t m = vi >> 8, e = vi & 255u;
+        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
+        const uint4 v4 = {v, v, v, v};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) row[(i + t) & 7u] = v4;
+        for (int i = 0; i < 8; ++i) row[(i + vi) & 7u] = v4;
+      }
     }
-    for (uint32_t i = t; i < 31u * 128u; i += kStageThreads)
-      reinterpret_cast<uint32_t*>(lds + kSNib)[i] = image[512 + i];
-    if (t == 0) *reinterpret_cast<uint32_t*>(lds + kSCtr) = 0;
+    if constexpr (LY::kNibInLds)
+      for (uint32_t i = t; i < 31u * 128u; i += kThreads)
+        reinterpret_cast<uint32_t*>(lds + LY::kNib)[i] = image[512 + i];
+    if (t == 0) *reinterpret_cast<uint32_t*>(lds + LY::kCtr) = 0;
   }
   __syncthreads();
   const uint64_t fb0 = (uint64_t)blockIdx.x * frames_per_wg;
@@ -159,8 +178,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint32_t nslice = (uint32_t)(fb1 - fb0);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t b0 = (lane & (FOLD == 4 ? 15u : 31u)) << 2;
-  char* tr = lds + kSTr + 8192u * wv;
-  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kSBnd + 1536u * wv);
+  char* tr = lds + LY::kTr + 8192u * wv;
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + 1536u * wv);
   constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
   const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<char*>(out) + fb0 * elem, (short)0, (int)(nslice * elem), 0x00020000);
@@ -169,7 +188,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 
   for (;;) {
     uint32_t blk = 0;
-    if (lane == 0) blk = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kSCtr), 1u, __ATOMIC_RELAXED,
+    if (lane == 0) blk = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + LY::kCtr), 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
     blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk);
     const uint64_t f0r = (uint64_t)blk * kStageBF;  // relative to fb0
@@ -422,7 +441,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       // stretches without a boundary (Jacobi sweeps until nothing changes)
       for (uint32_t it = 0; it < 64u; ++it) {
         const uint32_t Pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)Pk);
-        const uint32_t zq = s_zd(lds, hbp ? 0u : Q, Pp);
+        const uint32_t zq = s_zd<W>(lds, image, hbp ? 0u : Q, Pp);
         const uint32_t Pn = hbp ? Ep : zq ^ Ep;
         const bool ch = Pn != Pk;
         Pk = Pn;
@@ -430,7 +449,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       }
     }
     if (__builtin_amdgcn_ballot_w64(rec) != 0) {
-      const uint32_t S = rec_S ^ s_zd(lds, rec ? rec_d : 0u, Pk);
+      const uint32_t S = rec_S ^ s_zd<W>(lds, image, rec ? rec_d : 0u, Pk);
       const uint32_t crc = ~S;
       const uint32_t fr = (uint32_t)f0r + rec_j - 1u;
       if constexpr (MODE == StageMode::kCrc) {
@@ -446,20 +465,23 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, const void* image, int num_cus, hipStream_t stream) {
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   uint64_t grid = (n + kStageBF - 1) / kStageBF;
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const uint64_t per = (n + grid - 1) / grid;
   const uint32_t* img = static_cast<const uint32_t*>(image);
-#define LNX_STAGE(M, F)                                                                                      \
-  hipLaunchKernelGGL((crc32_stage_kernel<M, F>), dim3((unsigned)grid), dim3(kStageThreads), 0, stream, bytes, off, \
-                     n, per, img, out)
+#define LNX_STAGE(M, F, W)                                                                                  \
+  hipLaunchKernelGGL((crc32_stage_kernel<M, F, W>), dim3((unsigned)grid), dim3(W * 64), 0, stream, bytes, off, n, \
+                     per, img, out)
+#define LNX_STAGE_W(M, F) \
+  if (waves == 10) LNX_STAGE(M, F, 10); else LNX_STAGE(M, F, 8)
   if (fold == 4) {
-    if (verify) LNX_STAGE(StageMode::kVerify, 4); else LNX_STAGE(StageMode::kCrc, 4);
+    if (verify) { LNX_STAGE_W(StageMode::kVerify, 4); } else { LNX_STAGE_W(StageMode::kCrc, 4); }
   } else {
-    if (verify) LNX_STAGE(StageMode::kVerify, 2); else LNX_STAGE(StageMode::kCrc, 2);
+    if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
   }
+#undef LNX_STAGE_W
 #undef LNX_STAGE
   return hipGetLastError();
 }
