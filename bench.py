@@ -616,7 +616,7 @@ def main():
             "traffic": None,
             "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
-                       "search": "lnx::crc32_search_u_kernel<2>",
+                       "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
                        "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
             "kernel_ms": round(kern_ms, 4),
