@@ -79,26 +79,43 @@ __device__ __forceinline__ uint32_t s_z2(const char* lds, uint32_t v, uint32_t b
 }
 // FOLD 2: Z_1 is table B.  FOLD 4 (variants 302 / 303): the four Z_4 byte
 // tables in 16 bank columns, entry e of table k, column c at e << 8 | k << 6 |
-// c << 2 (64 KiB like FOLD 2's; lanes c and c + 16 share a column, so every
-// lookup is a 2-way bank conflict), one LDS round trip per dword instead of
-// two; Z_1 is its table 3 (Z_4(e << 24) = Z_1(e)).
+// c << 2 (64 KiB like FOLD 2's), one LDS round trip per dword instead of two;
+// Z_1 is its table 3 (Z_4(e << 24) = Z_1(e)).  Lanes c and c + 16 share column
+// c, and table k sits in bank half k & 1, so the k-th lookup of lane half h =
+// (lane >> 4) & 1 reads table (k + h) & 3: in every instruction the two halves
+// of a 32-lane pass read opposite bank halves (conflict-free; the XOR of the
+// four lookups does not depend on their order).
 template <int FOLD>
 __device__ __forceinline__ uint32_t s_z1(const char* lds, uint32_t v, uint32_t b0) {
   return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + (FOLD == 4 ? 192u : 128u));
 }
+// the FOLD 4 lookups' per-lane v_perm bases / selectors: lookup i reads table
+// k = (i + h) & 3 at byte (v.byte_k << 8) | (k << 6) | (c << 2)
+struct Z4Lane {
+  uint32_t base[4], sel[4];
+  __device__ explicit Z4Lane(uint32_t lane) {
+    const uint32_t h = (lane >> 4) & 1u, c = lane & 15u;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t k = (i + h) & 3u;
+      base[i] = (k << 6) | (c << 2);
+      sel[i] = 0x0c020400u + (k << 8);
+    }
+  }
+};
 // Z_4(v)
 template <int FOLD>
-__device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b0) {
+__device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b0, const Z4Lane& zl) {
   if constexpr (FOLD == 4) {
-    const uint32_t a0 = __builtin_amdgcn_perm(v, b0, 0x0c020400u), a1 = __builtin_amdgcn_perm(v, b0, 0x0c020500u);
-    const uint32_t a2 = __builtin_amdgcn_perm(v, b0, 0x0c020600u), a3 = __builtin_amdgcn_perm(v, b0, 0x0c020700u);
-    return __builtin_amdgcn_bitop3_b32(s_lds(lds, kSTab + a0), s_lds(lds, kSTab + a1 + 64u),
-                                       s_lds(lds, kSTab + a2 + 128u), 0x96) ^
-           s_lds(lds, kSTab + a3 + 192u);
+    uint32_t y[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v, zl.base[i], zl.sel[i]));
+    return __builtin_amdgcn_bitop3_b32(y[0], y[1], y[2], 0x96) ^ y[3];
   } else {
     return s_z2(lds, s_z2(lds, v, b0), b0);
   }
 }
+
 // Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
 // nibble value picks one of 16 banks, equal values broadcast), from LDS or,
 // for W > 8, from the image in HBM (dword (m, i, v) at 512 + 128 m + 16 i + v)
@@ -178,6 +195,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint32_t nslice = (uint32_t)(fb1 - fb0);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t b0 = (lane & (FOLD == 4 ? 15u : 31u)) << 2;
+  const Z4Lane zl(lane);
   char* tr = lds + LY::kTr + 8192u * wv;
   uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + 1536u * wv);
   constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
@@ -397,7 +415,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
           const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
           const uint32_t v = at ? vr : r ^ w;
-          r = s_z4<FOLD>(lds, v, b0);
+          r = s_z4<FOLD>(lds, v, b0, zl);
         }
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
           uint32_t S = ecap;  // Z_c(e), c = 0..3

@@ -16,7 +16,7 @@ for f in sorted(glob.glob(os.path.join(d, "pmc*", "pmc_counter_collection.csv"))
         k = r["Kernel_Name"]
         if "lnx::" not in k:
             continue
-        short = k.split("(")[0].replace("lnx::", "")
+        short = (k[:k.rfind(">(") + 1] if ">(" in k else k.split("(")[0]).replace("lnx::", "").replace("void ", "")
         c = r["Counter_Name"]
         vals[short][c] += float(r["Counter_Value"])
         disp[short][c].add(r["Dispatch_Id"])
