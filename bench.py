@@ -368,6 +368,9 @@ def main():
     ap.add_argument("--op", default="crc32",
                     choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search",
                              "tx_checksum", "egress_packets", "ingress_packets"])
+    ap.add_argument("--short-frames", action="store_true",
+                    help="--op crc32 / fcs_verify through lnx_*_batch_ex(LNX_BATCH_SHORT_FRAMES): the staged "
+                         "lane-stream kernel the caller picks for a short-frame mix (DESIGN.md §3.9)")
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
@@ -504,7 +507,7 @@ def main():
         elif args.op == "sum16":
             L.sum16_batch(d_bytes, d_seg, d_len, d_seed, out=d_sum, stream=stream)
         elif args.op == "fcs_verify":
-            L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+            L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream, short_frames=args.short_frames)
         elif args.op == "ingress":
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "tx_checksum":
@@ -516,7 +519,7 @@ def main():
                 d_len.copy_(d_len0, non_blocking=True)
             L.fcs_append_batch(d_bytes, d_start, d_len, 1536, status=d_status, stream=stream)
         else:
-            L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream)
+            L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream, short_frames=args.short_frames)
 
     # The first few hundred microseconds of launches on an idle GPU run at
     # ramping clocks (tools/prof/variants.py measured ~5 % slower kernels):
@@ -614,7 +617,9 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
+            "kernel": ({"crc32": "lnx::crc32_stage_kernel<kCrc, 4, 8>",
+                        "fcs_verify": "lnx::crc32_stage_kernel<kVerify, 4, 8>"} if args.short_frames else {}).get(
+                args.op) or {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
@@ -624,7 +629,9 @@ def main():
             "algorithmic_bytes_per_launch": nbytes,
         },
     }
-    tag = wname if args.op == "crc32" else f"{wname}_{args.op}"
+    tag = (wname if args.op == "crc32" else f"{wname}_{args.op}") + ("_short" if args.short_frames else "")
+    if args.short_frames:
+        out["config"]["entry"] = "lnx_crc32_batch_ex / lnx_fcs_verify_batch_ex with LNX_BATCH_SHORT_FRAMES"
     traffic_file = os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
     if os.path.exists(traffic_file):
         with open(traffic_file) as fh:

@@ -89,6 +89,21 @@ uint16_t lnx_never_zero_sum(uint16_t sum16);
 int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n,
                     uint32_t* d_crc, void* stream);
 
+/* lnx_crc32_batch / lnx_fcs_verify_batch with flags.  LNX_BATCH_SHORT_FRAMES:
+ * the caller knows the batch's mean frame length is short (under
+ * LNX_SHORT_FRAME_MEAN bytes, e.g. a receive ring holding the traffic's mix):
+ * the frames are read by the staged lane-stream kernel, which requests each
+ * 128-byte line once instead of per-frame windows.  Results
+ * are identical either way; the flag only picks the faster kernel for the mix
+ * (the library cannot see device-resident offsets without a sync).  Other
+ * bits must be 0. */
+#define LNX_BATCH_SHORT_FRAMES 1u
+#define LNX_SHORT_FRAME_MEAN 512u
+int lnx_crc32_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc, uint32_t flags,
+                       void* stream);
+int lnx_fcs_verify_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
+                            uint32_t flags, void* stream);
+
 /* Segment form of lnx_crc32_batch for frames that are not packed back to back
  * (ring slots): d_crc[i] = CRC32(d_bytes[d_start[i] : d_start[i] + d_len[i]]).
  * Frames must be in increasing address order and must not overlap. */

@@ -122,6 +122,8 @@ _sig = {
                                            _vp, _vp]),
     "lnx_ingress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                            _vp, _vp]),
+    "lnx_crc32_batch_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]),
+    "lnx_fcs_verify_batch_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]),
     "lnx_egress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
@@ -291,33 +293,49 @@ def _need_len(what, name, t, n):
         raise LnetoError(f"{what}: {name} holds {t.numel()} elements, {n} needed")
 
 
-def crc32_batch(d_bytes, d_off, out=None, stream=None):
+BATCH_SHORT_FRAMES = 1  # LNX_BATCH_SHORT_FRAMES
+SHORT_FRAME_MEAN = 512  # LNX_SHORT_FRAME_MEAN
+
+
+def crc32_batch(d_bytes, d_off, out=None, stream=None, short_frames=False):
     """CRC32 of every frame d_bytes[d_off[i]:d_off[i+1]] on the GPU.
 
     d_bytes: uint8 device tensor; d_off: int64 device tensor of N+1 offsets.
     Returns an int32 device tensor holding the uint32 CRCs bit-for-bit.
+    short_frames=True (lnx_crc32_batch_ex with LNX_BATCH_SHORT_FRAMES): the
+    caller knows the mean frame length is under SHORT_FRAME_MEAN bytes; the
+    staged lane-stream kernel reads the batch (same results).
     """
     import torch
-    what = "lnx_crc32_batch"
+    what = "lnx_crc32_batch_ex" if short_frames else "lnx_crc32_batch"
     b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
     out = _out(what, out, n, torch.int32, "i32", b.device)
     if n > 0:
         with b as s:
-            _check(lib.lnx_crc32_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
+            if short_frames:
+                _check(lib.lnx_crc32_batch_ex(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
+                                              BATCH_SHORT_FRAMES, s), what)
+            else:
+                _check(lib.lnx_crc32_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
     return out
 
 
-def fcs_verify_batch(d_bytes, d_off, out=None, stream=None):
-    """1 where frame i (payload + trailing LE FCS) passes the FCS check, else 0."""
+def fcs_verify_batch(d_bytes, d_off, out=None, stream=None, short_frames=False):
+    """1 where frame i (payload + trailing LE FCS) passes the FCS check, else 0
+    (short_frames as crc32_batch)."""
     import torch
-    what = "lnx_fcs_verify_batch"
+    what = "lnx_fcs_verify_batch_ex" if short_frames else "lnx_fcs_verify_batch"
     b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
     n = d_off.numel() - 1
     out = _out(what, out, n, torch.uint8, "u8", b.device)
     if n > 0:
         with b as s:
-            _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
+            if short_frames:
+                _check(lib.lnx_fcs_verify_batch_ex(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(),
+                                                   BATCH_SHORT_FRAMES, s), what)
+            else:
+                _check(lib.lnx_fcs_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
     return out
 
 

@@ -17,14 +17,14 @@
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                bool verify, const void* image, int num_cus, hipStream_t stream);
+hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
 #ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
                               uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
-hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
 #endif
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
@@ -295,16 +295,25 @@ int get_ctx(DeviceCtx** out) {
   return LNX_OK;
 }
 
+// The staged lane-stream form the product uses for LNX_BATCH_SHORT_FRAMES
+// (stage_kernel.hip): the Z_4 fold in 16 rotated bank columns,
+// 8 waves per workgroup.
+constexpr int kStageFold = 4, kStageWaves = 8;
+
 int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify,
-               void* stream) {
+               uint32_t flags, void* stream) {
+  if (flags & ~LNX_BATCH_SHORT_FRAMES) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   if (!d_bytes || !d_off || !d_out) return LNX_EINVAL;
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
-                                     static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "crc32_frames_kernel launch");
+  hipError_t e = (flags & LNX_BATCH_SHORT_FRAMES)
+                     ? launch_crc32_stage(d_bytes, d_off, n, d_out, verify, kStageFold, kStageWaves, c->d_stage,
+                                          c->num_cus, static_cast<hipStream_t>(stream))
+                     : launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
+                                           static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "crc32 batch launch");
   return LNX_OK;
 }
 
@@ -312,12 +321,13 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
 
 // For the other translation units (rx_ring.hip): the current device's LDS
 // image and CU count, and the thread's lnx_last_error.
-int device_resources(const void** image, int* num_cus) {
+int device_resources(const void** image, int* num_cus, const void** stage_image) {
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   *image = c->d_image;
   *num_cus = c->num_cus;
+  if (stage_image) *stage_image = c->d_stage;
   return LNX_OK;
 }
 int hip_error(hipError_t e, const char* what) { return hip_fail(e, what); }
@@ -330,12 +340,22 @@ extern "C" {
 
 int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
                     void* stream) {
-  return crc_common(d_bytes, d_off, n, d_crc, false, stream);
+  return crc_common(d_bytes, d_off, n, d_crc, false, 0, stream);
 }
 
 int lnx_fcs_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
                          void* stream) {
-  return crc_common(d_bytes, d_off, n, d_ok, true, stream);
+  return crc_common(d_bytes, d_off, n, d_ok, true, 0, stream);
+}
+
+int lnx_crc32_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc, uint32_t flags,
+                       void* stream) {
+  return crc_common(d_bytes, d_off, n, d_crc, false, flags, stream);
+}
+
+int lnx_fcs_verify_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
+                            uint32_t flags, void* stream) {
+  return crc_common(d_bytes, d_off, n, d_ok, true, flags, stream);
 }
 
 int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_t* d_len,
@@ -495,7 +515,10 @@ int lnx_crc32_batch_host(const uint8_t* h_bytes, uint64_t nbytes, const uint64_t
         (e = hipMemcpyAsync(d_off, h_off, (n + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
       rc = hip_fail(e, "hipMemcpyAsync H2D");
   }
-  if (rc == LNX_OK) rc = lnx_crc32_batch(d_bytes, d_off, n, d_crc, s);
+  // the host knows this batch's mix: short-frame batches take the staged kernel
+  const uint32_t flags = (h_off[n] > h_off[0] ? h_off[n] - h_off[0] : 0) < (uint64_t)n * LNX_SHORT_FRAME_MEAN
+                             ? LNX_BATCH_SHORT_FRAMES : 0u;
+  if (rc == LNX_OK) rc = lnx_crc32_batch_ex(d_bytes, d_off, n, d_crc, flags, s);
   if (rc == LNX_OK && (e = hipMemcpyAsync(h_crc, d_crc, n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     rc = hip_fail(e, "hipMemcpyAsync D2H");
   if (d_bytes) (void)hipFreeAsync(d_bytes, s);

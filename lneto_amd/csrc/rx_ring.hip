@@ -46,7 +46,9 @@
 
 namespace lnx {
 
-int device_resources(const void** image, int* num_cus);
+int device_resources(const void** image, int* num_cus, const void** stage_image);
+hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
 int hip_error(hipError_t e, const char* what);
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
                                const void* images, int num_cus, hipStream_t stream);
@@ -100,6 +102,7 @@ struct lnx_rx_ring {
   std::vector<Stage> st;
   RxFilter filt{};  // lnx_rx_ring_set_filter; on = 0: accept-all
   const void* image = nullptr;
+  const void* stage_image = nullptr;  // the staged lane streams' tables (short-frame batches)
   int num_cus = 0;
   std::mutex mu;  // one call at a time (the stages are shared)
 };
@@ -182,8 +185,13 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
     if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
         (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess)
       return hip_error(e, "rx ring H2D (packed)");
-    e = fcs ? launch_crc32_frames(s.d_bytes, s.d_start, nb, s.d_ok, true, r->image, r->num_cus, s.s)
-            : hipMemsetAsync(s.d_ok, 1, nb, s.s);
+    // a packed batch of short frames (the host knows its mix) takes the staged
+    // lane streams, a batch of long ones the row kernel
+    const bool short_mix = total < (uint64_t)nb * LNX_SHORT_FRAME_MEAN;
+    e = !fcs ? hipMemsetAsync(s.d_ok, 1, nb, s.s)
+        : short_mix ? launch_crc32_stage(s.d_bytes, s.d_start, nb, s.d_ok, true, 4, 8, r->stage_image, r->num_cus,
+                                         s.s)
+                    : launch_crc32_frames(s.d_bytes, s.d_start, nb, s.d_ok, true, r->image, r->num_cus, s.s);
     if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");
     if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, nullptr, trim,
                                    &r->filt)) != hipSuccess)
@@ -255,7 +263,7 @@ int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t 
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   auto* r = new lnx_rx_ring;
   r->device = device, r->nslots = nslots, r->cap = slot_cap, r->batch = batch_slots, r->depth = depth;
-  int rc = device_resources(&r->image, &r->num_cus);
+  int rc = device_resources(&r->image, &r->num_cus, &r->stage_image);
   if (rc != LNX_OK) { ring_free(r); return rc; }
   const size_t slots_bytes = (size_t)nslots * slot_cap;
   if ((e = hipHostMalloc(reinterpret_cast<void**>(&r->h_slots), slots_bytes, hipHostMallocDefault)) != hipSuccess ||

@@ -37,9 +37,6 @@
 #include <cstdint>
 
 namespace lnx {
-// research library only until it is measured against the product dispatch
-// (tools/prof/variants.py --var 300)
-#ifdef LNX_RESEARCH
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -492,6 +489,7 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
 #define LNX_STAGE(M, F, W)                                                                                  \
   hipLaunchKernelGGL((crc32_stage_kernel<M, F, W>), dim3((unsigned)grid), dim3(W * 64), 0, stream, bytes, off, n, \
                      per, img, out)
+#ifdef LNX_RESEARCH  // variants 300-307: both folds, 8 or 10 waves
 #define LNX_STAGE_W(M, F) \
   if (waves == 10) LNX_STAGE(M, F, 10); else LNX_STAGE(M, F, 8)
   if (fold == 4) {
@@ -500,9 +498,12 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
     if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
   }
 #undef LNX_STAGE_W
+#else  // the product form only
+  if (fold != 4 || waves != 8) return hipErrorInvalidValue;
+  if (verify) LNX_STAGE(StageMode::kVerify, 4, 8); else LNX_STAGE(StageMode::kCrc, 4, 8);
+#endif
 #undef LNX_STAGE
   return hipGetLastError();
 }
 
-#endif  // LNX_RESEARCH
 }  // namespace lnx

@@ -49,6 +49,9 @@ def test_batch_entry_points_validate_without_gpu():
     assert L.lib.lnx_fcs_verify_batch(None, None, 5, None, None) == L.LNX_EINVAL
     assert L.lib.lnx_sum16_batch(None, None, None, None, 5, None, None) == L.LNX_EINVAL
     assert L.lib.lnx_crc32_batch_multi(0, None, None, None, None, None) == L.LNX_EINVAL
+    assert L.lib.lnx_crc32_batch_ex(None, None, 5, None, L.BATCH_SHORT_FRAMES, None) == L.LNX_EINVAL
+    assert L.lib.lnx_crc32_batch_ex(None, None, 0, None, 2, None) == L.LNX_EINVAL  # unknown flag bit
+    assert L.lib.lnx_fcs_verify_batch_ex(None, None, 0, None, L.BATCH_SHORT_FRAMES, None) == 0
     buf = (ctypes.c_uint8 * 8)()
     off = (ctypes.c_uint64 * 2)(0, 100)  # offset beyond nbytes
     out = (ctypes.c_uint32 * 1)()
@@ -110,8 +113,10 @@ def test_product_library_holds_only_product_kernels():
         assert re.search(r"CrcModeE\dELi0E", k), k          # VAR = 0
         assert re.search(r"ELi0EEEvPKh", k), k              # STR = 0
     others = sorted(re.sub(r"^_ZN3lnx\d+(\w+?kernel).*$", r"\1", k) for k in ks if k not in rows)
-    assert others == ["crc32_search_o_kernel", "ingress_verify_kernel", "ingress_verify_kernel",
-                      "ring_segments_kernel", "sum16_lines_kernel"], others
+    assert others == ["crc32_search_o_kernel", "crc32_stage_kernel", "crc32_stage_kernel", "ingress_verify_kernel",
+                      "ingress_verify_kernel", "ring_segments_kernel", "sum16_lines_kernel"], others
+    stage = [k for k in ks if "crc32_stage_kernel" in k]
+    assert all(re.search(r"StageModeE\dELi4ELi8E", k) for k in stage), stage  # the product fold / wave count
     research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
     if os.path.exists(research):
         rk = _kernels(research)

@@ -133,3 +133,33 @@ def test_gpu_stage_verify(cuda, var):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, bad[:10]
     assert want.sum() > 100_000 and (want == 0).sum() > 50_000
+
+
+@pytest.mark.gpu
+def test_gpu_short_frames_entry(cuda):
+    """The product entry (lnx_crc32_batch_ex / lnx_fcs_verify_batch_ex with
+    LNX_BATCH_SHORT_FRAMES, and lnx_crc32_batch_host, which picks the staged
+    kernel itself for a short mix) against the oracle."""
+    import torch
+    import lneto_amd as L
+    from lneto_amd import synth
+    from oracle import oracle as O
+    rng = np.random.default_rng(51)
+    cases = [synth.offsets_from_lengths(synth.zipf_lengths(300_001, seed=3)),
+             np.concatenate([[0], synth.offsets_from_lengths(rng.permutation(np.arange(0, 701))) + 5]),
+             np.concatenate([[0], synth.offsets_from_lengths(rng.choice([0, 1, 3, 17, 64, 65], size=30000)) + 1])]
+    for k, off in enumerate(cases):
+        off = np.asarray(off, dtype=np.int64)
+        data = synth.bytes_np(int(off[-1]) + 8, seed=60 + k)
+        want = O.crc32_frames(data, off.astype(np.uint64), threads=8)
+        d = torch.from_numpy(data).to(cuda)
+        o = torch.from_numpy(off).to(cuda)
+        got = L.crc32_batch(d, o, short_frames=True).cpu().numpy().view(np.uint32)
+        assert (got == want).all(), (k, np.nonzero(got != want)[0][:8])
+        ok = L.fcs_verify_batch(d, o, short_frames=True).cpu().numpy()
+        lens = np.diff(off)
+        assert (ok == ((want == 0x2144DF1C) & (lens >= 4))).all(), k
+        host = np.zeros(len(off) - 1, dtype=np.uint32)
+        assert L.lib.lnx_crc32_batch_host(data.ctypes.data, data.size, off.astype(np.uint64).ctypes.data,
+                                          len(off) - 1, host.ctypes.data, 0) == 0
+        assert (host == want).all(), k
