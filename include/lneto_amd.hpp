@@ -86,13 +86,16 @@ inline int CRC32Search(Bytes data, int minOffCRC) {
 }
 
 // Batch extensions over packed frames (device pointers).
+// flags: LNX_BATCH_SHORT_FRAMES for a short-frame mix (the staged lane-stream kernel).
 inline int CRC32Batch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint32_t* d_crc,
-                      void* stream = nullptr) {
-  return lnx_crc32_batch(d_frames, d_off, n, d_crc, stream);
+                      void* stream = nullptr, uint32_t flags = 0) {
+  return flags ? lnx_crc32_batch_ex(d_frames, d_off, n, d_crc, flags, stream)
+               : lnx_crc32_batch(d_frames, d_off, n, d_crc, stream);
 }
 inline int VerifyFCSBatch(const uint8_t* d_frames, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
-                          void* stream = nullptr) {
-  return lnx_fcs_verify_batch(d_frames, d_off, n, d_ok, stream);
+                          void* stream = nullptr, uint32_t flags = 0) {
+  return flags ? lnx_fcs_verify_batch_ex(d_frames, d_off, n, d_ok, flags, stream)
+               : lnx_fcs_verify_batch(d_frames, d_off, n, d_ok, stream);
 }
 // Frames in ring slots: CRC32 of bytes[start[i] : start[i] + len[i]].
 inline int CRC32Segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
