@@ -18,7 +18,8 @@ namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                bool verify, const void* image, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
+                              bool big_blocks = false);
 #ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
@@ -565,10 +566,12 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   if (st != LNX_OK) return st;
   // 300 / 301: the staged lane streams (stage_kernel.hip), CRC / FCS verify,
   // slicing-by-2 fold; 302 / 303: the same with the 16-column Z_4 fold;
-  // 304-307: 300-303 with 10 waves per workgroup instead of 8
-  hipError_t e = var >= 300 && var <= 307
-                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1, (var & 2) ? 4 : 2, var >= 304 ? 10 : 8,
-                                          c->d_stage, c->num_cus, static_cast<hipStream_t>(stream))
+  // 304-307: 300-303 with 10 waves per workgroup instead of 8; 308 / 309:
+  // 302 / 303 with 766-frame blocks
+  hipError_t e = var >= 300 && var <= 309
+                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1, (var & 2) || var >= 308 ? 4 : 2,
+                                          var >= 304 && var < 308 ? 10 : 8, c->d_stage, c->num_cus,
+                                          static_cast<hipStream_t>(stream), var >= 308)
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,
                                             static_cast<hipStream_t>(stream), nullptr);
   if (e != hipSuccess) return hip_fail(e, "crc32 variant launch");

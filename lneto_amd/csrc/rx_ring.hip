@@ -48,7 +48,8 @@ namespace lnx {
 
 int device_resources(const void** image, int* num_cus, const void** stage_image);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream);
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
+                              bool big_blocks = false);
 int hip_error(hipError_t e, const char* what);
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
                                const void* images, int num_cus, hipStream_t stream);

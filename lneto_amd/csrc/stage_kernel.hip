@@ -43,17 +43,20 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 enum class StageMode : int { kCrc = 0, kVerify = 1 };
 
 constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
+constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, half the per-block overhead
 // LDS layout (bytes) for W waves per workgroup.  W = 8: the Z_{2^m} nibble
 // tables live in LDS too; W = 10 (variants 304-307): they are read from the
 // image in HBM (only the carries use them, once per stretch), which frees the
 // room for two more waves' transposes and lists.
 constexpr uint32_t kSTab = 0;  // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
-template <int W>
+template <int W, uint32_t BF = kStageBF>
 struct StageLds {
+  static_assert((BF + 2) % 64 == 0, "whole-wave list loads");
+  static constexpr uint32_t kList = (BF + 2) * 4;      // boundary list bytes per wave (bf + 1 entries + sentinel)
   static constexpr uint32_t kTr = 65536;               // transposes: 8 KiB per wave
-  static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists: 1536 B per wave
-  static constexpr bool kNibInLds = W <= 8;
-  static constexpr uint32_t kNib = kBnd + W * 1536;    // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
+  static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists
+  static constexpr bool kNibInLds = kBnd + W * kList + 31 * 512 + 16 <= 163840;
+  static constexpr uint32_t kNib = kBnd + W * kList;   // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
   static constexpr uint32_t kCtr = kNib + (kNibInLds ? 31 * 512 : 0);  // the workgroup's block counter
   static constexpr uint32_t kBytes = kCtr + 16;
   static_assert(kBytes <= 163840, "stage LDS");
@@ -116,11 +119,11 @@ __device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b
 // Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
 // nibble value picks one of 16 banks, equal values broadcast), from LDS or,
 // for W > 8, from the image in HBM (dword (m, i, v) at 512 + 128 m + 16 i + v)
-template <int W>
+template <class LY>
 __device__ __forceinline__ uint32_t s_zpow2(const char* lds, const uint32_t* image, uint32_t m, uint32_t v) {
   uint32_t a = 0;
-  if constexpr (StageLds<W>::kNibInLds) {
-    const uint32_t t = StageLds<W>::kNib + 512u * m;
+  if constexpr (LY::kNibInLds) {
+    const uint32_t t = LY::kNib + 512u * m;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
   } else {
@@ -131,10 +134,10 @@ __device__ __forceinline__ uint32_t s_zpow2(const char* lds, const uint32_t* ima
   return a;
 }
 // Z_d(v), d < 2^31, by binary powers; lanes whose d is done keep their value
-template <int W>
+template <class LY>
 __device__ __forceinline__ uint32_t s_zd(const char* lds, const uint32_t* image, uint32_t d, uint32_t v) {
   for (uint32_t m = 0; __builtin_amdgcn_ballot_w64((d >> m) != 0u) != 0; ++m) {
-    const uint32_t z = s_zpow2<W>(lds, image, m, v);
+    const uint32_t z = s_zpow2<LY>(lds, image, m, v);
     v = ((d >> m) & 1u) ? z : v;
   }
   return v;
@@ -151,11 +154,12 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE, int FOLD, int W>
+template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF>
 __global__ void __launch_bounds__(W * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
-  using LY = StageLds<W>;
+  using LY = StageLds<W, BF>;
+  constexpr uint32_t kLast = BF + 1;  // the list's last entry (a sentinel past bf)
   constexpr uint32_t kThreads = W * 64;
   __shared__ __attribute__((aligned(16))) char lds[LY::kBytes];
   // ---- image: A / B values expanded into their 32 bank columns (FOLD 4: the
@@ -194,7 +198,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint32_t b0 = (lane & (FOLD == 4 ? 15u : 31u)) << 2;
   const Z4Lane zl(lane);
   char* tr = lds + LY::kTr + 8192u * wv;
-  uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + 1536u * wv);
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + LY::kList * wv);
   constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
   const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<char*>(out) + fb0 * elem, (short)0, (int)(nslice * elem), 0x00020000);
@@ -206,9 +210,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     if (lane == 0) blk = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + LY::kCtr), 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
     blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk);
-    const uint64_t f0r = (uint64_t)blk * kStageBF;  // relative to fb0
+    const uint64_t f0r = (uint64_t)blk * BF;  // relative to fb0
     if (f0r >= nslice) break;
-    const uint32_t bf = (uint32_t)(nslice - f0r < kStageBF ? nslice - f0r : kStageBF);
+    const uint32_t bf = (uint32_t)(nslice - f0r < BF ? nslice - f0r : BF);
     const uint64_t f0 = fb0 + f0r;
     const uint64_t A = off[f0], E = off[f0 + bf];
     const uint8_t* pa = bytes + A;
@@ -216,7 +220,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     const uint64_t span = E > A ? E - A + adj : adj;
     // ---- boundary list (relative to the line-aligned base): x_j = off[f0 + j] - A + adj
 #pragma unroll
-    for (uint32_t i = 0; i < 6u; ++i) {  // (six whole-wave loads: entry j > bf re-reads entry bf)
+    for (uint32_t i = 0; i < (BF + 2) / 64; ++i) {  // (whole-wave loads: entry j > bf re-reads entry bf)
       const uint32_t j = lane + 64u * i;
       const uint64_t o = off[f0 + (j <= bf ? j : bf)];
       const uint32_t x = o > A ? (uint32_t)(o - A) + adj : adj;  // (non-decreasing offsets: o >= A)
@@ -267,14 +271,14 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     uint32_t lo = 0, hi = bf + 1u;
     while (__builtin_amdgcn_ballot_w64(lo < hi) != 0) {
       const uint32_t mid = (lo + hi) >> 1;
-      const uint32_t xm = list[mid < 383u ? mid : 383u];
+      const uint32_t xm = list[mid < kLast ? mid : kLast];
       if (lo < hi) {
         if (xm >= Sk) hi = mid; else lo = mid + 1u;
       }
     }
     const uint32_t jstart = lo;
     uint32_t j = lo;
-    uint32_t x = list[j], x1 = list[j + 1u < 383u ? j + 1u : 383u];  // (j = bf + 1 past the block end)
+    uint32_t x = list[j], x1 = list[j + 1u < kLast ? j + 1u : kLast];  // (j = bf + 1 past the block end)
     uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
     uint32_t r = 0;
     bool first = true;
@@ -356,7 +360,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       xprev = ev ? x : xprev;
       j = ev ? j + 1u : j;
       x = ev ? x1 : x;
-      const uint32_t x2 = list[j + 1u < 383u ? j + 1u : 383u];
+      const uint32_t x2 = list[j + 1u < kLast ? j + 1u : kLast];
       x1 = ev ? x2 : x1;
     };
 
@@ -456,7 +460,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       // stretches without a boundary (Jacobi sweeps until nothing changes)
       for (uint32_t it = 0; it < 64u; ++it) {
         const uint32_t Pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)Pk);
-        const uint32_t zq = s_zd<W>(lds, image, hbp ? 0u : Q, Pp);
+        const uint32_t zq = s_zd<LY>(lds, image, hbp ? 0u : Q, Pp);
         const uint32_t Pn = hbp ? Ep : zq ^ Ep;
         const bool ch = Pn != Pk;
         Pk = Pn;
@@ -464,7 +468,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       }
     }
     if (__builtin_amdgcn_ballot_w64(rec) != 0) {
-      const uint32_t S = rec_S ^ s_zd<W>(lds, image, rec ? rec_d : 0u, Pk);
+      const uint32_t S = rec_S ^ s_zd<LY>(lds, image, rec ? rec_d : 0u, Pk);
       const uint32_t crc = ~S;
       const uint32_t fr = (uint32_t)f0r + rec_j - 1u;
       if constexpr (MODE == StageMode::kCrc) {
@@ -480,26 +484,31 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream) {
+                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
+                              bool big_blocks) {
   if (n == 0) return hipSuccess;
-  uint64_t grid = (n + kStageBF - 1) / kStageBF;
+  const uint64_t bfl = big_blocks ? kStageBFBig : kStageBF;
+  uint64_t grid = (n + bfl - 1) / bfl;
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const uint64_t per = (n + grid - 1) / grid;
   const uint32_t* img = static_cast<const uint32_t*>(image);
-#define LNX_STAGE(M, F, W)                                                                                  \
-  hipLaunchKernelGGL((crc32_stage_kernel<M, F, W>), dim3((unsigned)grid), dim3(W * 64), 0, stream, bytes, off, n, \
-                     per, img, out)
-#ifdef LNX_RESEARCH  // variants 300-307: both folds, 8 or 10 waves
+#define LNX_STAGE(M, F, W, ...)                                                                             \
+  hipLaunchKernelGGL((crc32_stage_kernel<M, F, W, ##__VA_ARGS__>), dim3((unsigned)grid), dim3(W * 64), 0, stream, \
+                     bytes, off, n, per, img, out)
+#ifdef LNX_RESEARCH  // variants 300-309: both folds, 8 or 10 waves, 382- or 766-frame blocks
 #define LNX_STAGE_W(M, F) \
   if (waves == 10) LNX_STAGE(M, F, 10); else LNX_STAGE(M, F, 8)
-  if (fold == 4) {
+  if (big_blocks) {
+    if (fold != 4 || waves != 8) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 4, 8, kStageBFBig); else LNX_STAGE(StageMode::kCrc, 4, 8, kStageBFBig);
+  } else if (fold == 4) {
     if (verify) { LNX_STAGE_W(StageMode::kVerify, 4); } else { LNX_STAGE_W(StageMode::kCrc, 4); }
   } else {
     if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
   }
 #undef LNX_STAGE_W
 #else  // the product form only
-  if (fold != 4 || waves != 8) return hipErrorInvalidValue;
+  if (fold != 4 || waves != 8 || big_blocks) return hipErrorInvalidValue;
   if (verify) LNX_STAGE(StageMode::kVerify, 4, 8); else LNX_STAGE(StageMode::kCrc, 4, 8);
 #endif
 #undef LNX_STAGE
