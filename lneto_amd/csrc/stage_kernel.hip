@@ -278,7 +278,10 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     }
     const uint32_t jstart = lo;
     uint32_t j = lo;
+    // the lane's next three boundaries: x (due), x1 (the slow-half test), x2
+    // (read one advance ahead, so that an advance never waits for the list)
     uint32_t x = list[j], x1 = list[j + 1u < kLast ? j + 1u : kLast];  // (j = bf + 1 past the block end)
+    uint32_t x2 = list[j + 2u < kLast ? j + 2u : kLast];
     uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
     uint32_t r = 0;
     bool first = true;
@@ -360,8 +363,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       xprev = ev ? x : xprev;
       j = ev ? j + 1u : j;
       x = ev ? x1 : x;
-      const uint32_t x2 = list[j + 1u < kLast ? j + 1u : kLast];
       x1 = ev ? x2 : x1;
+      const uint32_t x3 = list[j + 2u < kLast ? j + 2u : kLast];
+      x2 = ev ? x3 : x2;
     };
 
     // one round: wait for the slot, stage its pieces in LDS, flush the held
@@ -375,14 +379,13 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
       flush();
       issue(cur, rr + 2u);
+      // the lane's whole line in one LDS round trip (both halves)
+      u32x4 ql[8];
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) ql[i] = *reinterpret_cast<const u32x4*>(tr + rb + 16u * ((i + rot) & 7u));
 #pragma unroll
       for (uint32_t h = 0; h < 2; ++h) {
-        u32x4 q[4];
-#pragma unroll
-        for (uint32_t i = 0; i < 4; ++i) {
-          const uint32_t pi = 4u * h + i;
-          q[i] = *reinterpret_cast<const u32x4*>(tr + rb + 16u * ((pi + rot) & 7u));
-        }
+        const u32x4* q = ql + 4 * h;
         const uint32_t P = Sk + 128u * rr + 64u * h;
         const uint32_t rel = x - P;
         const bool in = rel < 64u;
@@ -420,10 +423,22 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
         }
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
           uint32_t S = ecap;  // Z_c(e), c = 0..3
+          if constexpr (FOLD == 4) {
+            // one round trip: Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e),
+            // Z_m(b) = Z_4(b << 8 (4 - m)) = table 4 - m's entry b
+            uint32_t y[3];
 #pragma unroll
-          for (uint32_t s = 0; s < 3; ++s) {
-            const uint32_t z = s_z1<FOLD>(lds, S, b0);
-            S = s < c ? z : S;
+            for (uint32_t i = 0; i < 3; ++i)
+              y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(ecap, b0, 0x0c020400u + (i << 8)) +
+                                    (((4u - c + i) & 3u) << 6));
+            const uint32_t sh = c == 0u ? ecap : ecap >> (8u * c);
+            S = __builtin_amdgcn_bitop3_b32(sh, c > 0u ? y[0] : 0u, c > 1u ? y[1] : 0u, 0x96) ^ (c > 2u ? y[2] : 0u);
+          } else {
+#pragma unroll
+            for (uint32_t s = 0; s < 3; ++s) {
+              const uint32_t z = s_z1<FOLD>(lds, S, b0);
+              S = s < c ? z : S;
+            }
           }
           end_at(in, S, x, (int)h);
           advance(in);
@@ -495,9 +510,11 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
 #define LNX_STAGE(M, F, W, ...)                                                                             \
   hipLaunchKernelGGL((crc32_stage_kernel<M, F, W, ##__VA_ARGS__>), dim3((unsigned)grid), dim3(W * 64), 0, stream, \
                      bytes, off, n, per, img, out)
-#ifdef LNX_RESEARCH  // variants 300-309: both folds, 8 or 10 waves, 382- or 766-frame blocks
-#define LNX_STAGE_W(M, F) \
-  if (waves == 10) LNX_STAGE(M, F, 10); else LNX_STAGE(M, F, 8)
+#ifdef LNX_RESEARCH  // variants 300-303, 308, 309: both folds, 382- or 766-frame blocks
+  // (10 waves per workgroup, variants 304-307, measured no faster in round 4
+  // and no longer fit its registers once the whole line is read at once)
+  if (waves != 8) return hipErrorInvalidValue;
+#define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
   if (big_blocks) {
     if (fold != 4 || waves != 8) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 4, 8, kStageBFBig); else LNX_STAGE(StageMode::kCrc, 4, 8, kStageBFBig);
