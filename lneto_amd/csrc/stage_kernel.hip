@@ -65,6 +65,9 @@ struct StageLds {
 // nibble tables verbatim (512 + 31 * 128 dwords), then (FOLD 4) the four Z_4
 // byte tables, table k entry e at kStageZ4Img + 256 k + e
 constexpr uint32_t kStageZ4Img = 512 + 31 * 128;
+// then (FOLD 8) the eight slicing-by-8 byte tables T8_k[e] = Z_{8-k}(e), table
+// k entry e at kStageZ8Img + 256 k + e
+constexpr uint32_t kStageZ8Img = kStageZ4Img + 1024;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -87,7 +90,36 @@ __device__ __forceinline__ uint32_t s_z2(const char* lds, uint32_t v, uint32_t b
 // four lookups does not depend on their order).
 template <int FOLD>
 __device__ __forceinline__ uint32_t s_z1(const char* lds, uint32_t v, uint32_t b0) {
-  return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + (FOLD == 4 ? 192u : 128u));
+  return (v >> 8) ^
+         s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + (FOLD == 8 ? 224u : FOLD == 4 ? 192u : 128u));
+}
+// FOLD 8 (variants 310 / 311): slicing-by-8 over 8-byte units, the eight byte
+// tables T8_k[e] = Z_{8-k}(e) in 8 bank columns, entry e of table k, column c
+// at e << 8 | k << 5 | c << 2 (64 KiB).  A unit (w0, w1) entered with r leaves
+// Z_8(r ^ w0) ^ Z_4(w1) = XOR_k T8_k[byte k of r ^ w0] ^ XOR_k T8_{4+k}[byte k
+// of w1]: the w1 half is off the chain, so a lane's chain takes one LDS round
+// trip per 8 bytes.  Table k sits in bank octet k & 3; the four 8-lane groups
+// g = (lane >> 3) & 3 of a pass read tables (i + g) & 3 (and 4 + that) in
+// lookup i, so each lookup instruction is conflict-free.
+struct Z8Lane {
+  uint32_t base[8], sel[4];  // base[i] (table (i + g) & 3), base[4 + i] (table 4 + ((i + g) & 3))
+  __device__ explicit Z8Lane(uint32_t lane) {
+    const uint32_t g = (lane >> 3) & 3u, c = lane & 7u;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t k = (i + g) & 3u;
+      base[i] = (k << 5) | (c << 2);
+      base[4 + i] = ((4u + k) << 5) | (c << 2);
+      sel[i] = 0x0c020400u + (k << 8);
+    }
+  }
+};
+// XOR_k T8_{4h+k}[byte k of v]: h = 0 the r-side half of Z_8, h = 1 Z_4(v)
+__device__ __forceinline__ uint32_t s_z8half(const char* lds, uint32_t v, const Z8Lane& z8, uint32_t h) {
+  uint32_t y[4];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v, z8.base[4 * h + i], z8.sel[i]));
+  return __builtin_amdgcn_bitop3_b32(y[0], y[1], y[2], 0x96) ^ y[3];
 }
 // the FOLD 4 lookups' per-lane v_perm bases / selectors: lookup i reads table
 // k = (i + h) & 3 at byte (v.byte_k << 8) | (k << 6) | (c << 2)
@@ -166,7 +198,15 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   // Z_4 values into 16), nibble tables verbatim
   {
     const uint32_t t = threadIdx.x;
-    if constexpr (FOLD == 4) {
+    if constexpr (FOLD == 8) {
+      for (uint32_t vi = t; vi < 2048u; vi += kThreads) {
+        const uint32_t v = image[kStageZ8Img + vi];
+        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 5));
+        const uint4 v4 = {v, v, v, v};
+        row[0] = v4;
+        row[1] = v4;
+      }
+    } else if constexpr (FOLD == 4) {
       for (uint32_t vi = t; vi < 1024u; vi += kThreads) {
         const uint32_t v = image[kStageZ4Img + vi];
         uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 6));
@@ -195,7 +235,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint64_t fb1 = fb0 + frames_per_wg < nframes ? fb0 + frames_per_wg : nframes;
   const uint32_t nslice = (uint32_t)(fb1 - fb0);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t b0 = (lane & (FOLD == 4 ? 15u : 31u)) << 2;
+  const uint32_t b0 = (lane & (FOLD == 8 ? 7u : FOLD == 4 ? 15u : 31u)) << 2;
+  const Z8Lane z8(lane);
   const Z4Lane zl(lane);
   char* tr = lds + LY::kTr + 8192u * wv;
   uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + LY::kList * wv);
@@ -412,18 +453,47 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
         const uint32_t lm = in ? (uint32_t)((1ull << (8u * c)) - 1ull) : 0u;
         const uint32_t Kc = c == 0u ? 0xFFFFFFFFu : c == 1u ? kK1 : c == 2u ? kK2 : kK3;
         uint32_t ecap = 0;
+        if constexpr (FOLD == 8) {
+          // 8-byte units; the unit holding the boundary captures (r, w0, w1)
+          uint32_t rc = 0, w0c = 0, w1c = 0;
 #pragma unroll
-        for (uint32_t d = 0; d < 16; ++d) {
-          const uint32_t w = q[d >> 2][d & 3u];
-          const bool at = d == kb;
-          ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
-          const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
-          const uint32_t v = at ? vr : r ^ w;
-          r = s_z4<FOLD>(lds, v, b0, zl);
+          for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
+            const bool a0 = 2u * u == kb, a1 = 2u * u + 1u == kb, au = a0 || a1;
+            rc = au ? r : rc, w0c = au ? w0 : w0c, w1c = au ? w1 : w1c;
+            const uint32_t v0 = a0 ? __builtin_amdgcn_bitop3_b32(w0, lm, Kc, 0x9A) : r ^ w0;
+            const uint32_t v1 = a1 ? __builtin_amdgcn_bitop3_b32(w1, lm, Kc, 0x9A) : w1;
+            const uint32_t yw = s_z8half(lds, v1, z8, 1);  // Z_4(v1): off the chain
+            const uint32_t yr = s_z8half(lds, v0, z8, 0);
+            r = (a1 ? 0u : yr) ^ yw;  // a new frame in w1 owes nothing to r
+          }
+          // the ending frame's state before Z_c: in w0, r ^ (w0 & lm); in w1,
+          // Z_4(r ^ w0) ^ (w1 & lm) (Z_4 = the T8_4..7 half)
+          const uint32_t z4t = s_z8half(lds, rc ^ w0c, z8, 1);
+          ecap = (kb & 1u) ? z4t ^ (w1c & lm) : rc ^ (w0c & lm);
+        } else {
+#pragma unroll
+          for (uint32_t d = 0; d < 16; ++d) {
+            const uint32_t w = q[d >> 2][d & 3u];
+            const bool at = d == kb;
+            ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
+            const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
+            const uint32_t v = at ? vr : r ^ w;
+            r = s_z4<FOLD>(lds, v, b0, zl);
+          }
         }
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
           uint32_t S = ecap;  // Z_c(e), c = 0..3
-          if constexpr (FOLD == 4) {
+          if constexpr (FOLD == 8) {
+            // Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e) = ... T8_{8-c+i}[byte i]
+            uint32_t y[3];
+#pragma unroll
+            for (uint32_t i = 0; i < 3; ++i)
+              y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(ecap, b0, 0x0c020400u + (i << 8)) +
+                                    (((8u - c + i) & 7u) << 5));
+            const uint32_t sh = c == 0u ? ecap : ecap >> (8u * c);
+            S = __builtin_amdgcn_bitop3_b32(sh, c > 0u ? y[0] : 0u, c > 1u ? y[1] : 0u, 0x96) ^ (c > 2u ? y[2] : 0u);
+          } else if constexpr (FOLD == 4) {
             // one round trip: Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e),
             // Z_m(b) = Z_4(b << 8 (4 - m)) = table 4 - m's entry b
             uint32_t y[3];
@@ -515,7 +585,10 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   // and no longer fit its registers once the whole line is read at once)
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (big_blocks) {
+  if (fold == 8) {
+    if (big_blocks) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8); else LNX_STAGE(StageMode::kCrc, 8, 8);
+  } else if (big_blocks) {
     if (fold != 4 || waves != 8) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 4, 8, kStageBFBig); else LNX_STAGE(StageMode::kCrc, 4, 8, kStageBFBig);
   } else if (fold == 4) {

@@ -69,3 +69,45 @@ def test_wave_simulation_matches_zlib(kind):
     want = S.zlib_crcs(data, off)
     got = SIM.stage_block_sim(data, off, 0, len(lens), 0)
     assert [got.get(i) for i in range(len(lens))] == want
+
+
+def test_slicing_by_8_unit_algebra():
+    """FOLD 8 (variants 310 / 311): an 8-byte unit (w0, w1) entered with r
+    leaves XOR_k T8_k[byte k of v0] ^ XOR_k T8_{4+k}[byte k of v1], T8_k[e] =
+    Z_{8-k}(e), with v0 = r ^ w0 (or the reset value when a frame starts in w0)
+    and v1 = w1 (or the reset value, the r side then dropped); the ending
+    frame's pre-Z_c state is r ^ (w0 & lm) in w0 and Z_4(r ^ w0) ^ (w1 & lm) in
+    w1; Z_c(e) = (e >> 8c) ^ XOR_{i<c} T8_{8-c+i}[byte i of e]."""
+    rng = random.Random(88)
+    T8 = [[S.zc(8 - k, e) for e in range(256)] for k in range(8)]
+
+    def half(v, h):
+        out = 0
+        for k in range(4):
+            out ^= T8[4 * h + k][(v >> (8 * k)) & 0xFF]
+        return out
+
+    for _ in range(3000):
+        r, w0, w1 = (rng.getrandbits(32) for _ in range(3))
+        # plain unit = two Z_4 steps
+        assert half(r ^ w0, 0) ^ half(w1, 1) == S.z4(S.z4(r ^ w0) ^ w1)
+        for where in (0, 1):
+            c = rng.randrange(4)
+            lm = (1 << (8 * c)) - 1
+            w = w0 if where == 0 else w1
+            vr = (w & ~lm & S.MASK) ^ S.K[c]
+            if where == 0:
+                got = half(vr, 0) ^ half(w1, 1)
+                want = S.z4(S.z4(vr) ^ w1)
+                e = r ^ (w0 & lm)
+                e_ref = r ^ (w0 & lm)
+            else:
+                got = half(w1 if False else vr, 1)
+                want = S.z4(vr)
+                e = half(r ^ w0, 1) ^ (w1 & lm)
+                e_ref = S.z4(r ^ w0) ^ (w1 & lm)
+            assert got == want and e == e_ref
+            zc = (e >> (8 * c)) if c else e
+            for i in range(c):
+                zc ^= T8[8 - c + i][(e >> (8 * i)) & 0xFF]
+            assert zc == S.zc(c, e)
