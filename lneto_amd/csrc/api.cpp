@@ -299,9 +299,9 @@ int get_ctx(DeviceCtx** out) {
 }
 
 // The staged lane-stream form the product uses for LNX_BATCH_SHORT_FRAMES
-// (stage_kernel.hip): the Z_4 fold in 16 rotated bank columns,
-// 8 waves per workgroup.
-constexpr int kStageFold = 4, kStageWaves = 8;
+// (stage_kernel.hip): the slicing-by-8 fold in 8 rotated bank
+// columns, 8 waves per workgroup.
+constexpr int kStageFold = 8, kStageWaves = 8;
 
 int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify,
                uint32_t flags, void* stream) {
@@ -650,7 +650,8 @@ const char* lnx_version(void) {
          "clients' checks) and TX checksum generate (the same rows, GEN) + rx ring (ingress and egress packets) + "
          "CRC32Search (eight captures per wave, 192-byte lane segments as four 48-byte chains joined by "
          "lane-private Z_48 nibble tables, 3-level scan, Z_4 in the lane-private U layout, pass B by word checks, "
-         "group-descriptor loads)";
+         "group-descriptor loads) + staged lane streams for short-frame batches (slicing-by-8 fold, LDS transposed "
+         "whole-line loads)";
 }
 
 }  // extern "C"

@@ -190,7 +190,7 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
     // lane streams, a batch of long ones the row kernel
     const bool short_mix = total < (uint64_t)nb * LNX_SHORT_FRAME_MEAN;
     e = !fcs ? hipMemsetAsync(s.d_ok, 1, nb, s.s)
-        : short_mix ? launch_crc32_stage(s.d_bytes, s.d_start, nb, s.d_ok, true, 4, 8, r->stage_image, r->num_cus,
+        : short_mix ? launch_crc32_stage(s.d_bytes, s.d_start, nb, s.d_ok, true, 8, 8, r->stage_image, r->num_cus,
                                          s.s)
                     : launch_crc32_frames(s.d_bytes, s.d_start, nb, s.d_ok, true, r->image, r->num_cus, s.s);
     if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");

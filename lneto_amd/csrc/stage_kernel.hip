@@ -597,9 +597,9 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
     if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
   }
 #undef LNX_STAGE_W
-#else  // the product form only
-  if (fold != 4 || waves != 8 || big_blocks) return hipErrorInvalidValue;
-  if (verify) LNX_STAGE(StageMode::kVerify, 4, 8); else LNX_STAGE(StageMode::kCrc, 4, 8);
+#else  // the product form only: the slicing-by-8 fold, 8 waves, 382-frame blocks
+  if (fold != 8 || waves != 8 || big_blocks) return hipErrorInvalidValue;
+  if (verify) LNX_STAGE(StageMode::kVerify, 8, 8); else LNX_STAGE(StageMode::kCrc, 8, 8);
 #endif
 #undef LNX_STAGE
   return hipGetLastError();
