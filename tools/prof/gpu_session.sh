@@ -11,7 +11,7 @@
 #   bench             the default bench line (what the driver runs)
 #   lines             a --verify'd bench line per workload / op
 #   line:WL:OP[:ARGS] one bench line (ARGS: extra flags, comma-separated)
-#   prof:WL[:OP]      rocprofv3 kernel trace + PMC passes (tools/prof/profile.sh)
+#   prof:WL[:OP[:short]] rocprofv3 kernel trace + PMC passes (tools/prof/profile.sh)
 #   py:FILE[:ARGS]    python FILE (a measurement script), ARGS comma-separated
 #   sh:FILE[:ARGS]    bash FILE (a measurement script), ARGS comma-separated
 set -o pipefail
@@ -51,7 +51,7 @@ for STEP in "$@"; do
       EXTRA=${C//,/ }
       run 300 $O/bench_${A}_${B}.jsonl python -u bench.py --workload $A --op $B $EXTRA
       tail -1 $O/bench_${A}_${B}.jsonl ;;
-    prof) run 900 $O/prof_${A}_${B:-crc32}.log bash tools/prof/profile.sh $TAG $A ${B:-crc32} ;;
+    prof) run 900 $O/prof_${A}_${B:-crc32}.log bash tools/prof/profile.sh $TAG $A ${B:-crc32} $C ;;
     py)  # a python script, or an executable (a microbenchmark binary built in-tree)
       if [[ $A == *.py ]]; then run 600 $O/py_$(basename $A .py).log python -u $A ${B//,/ };
       else run 600 $O/py_$(basename $A).log ./$A ${B//,/ }; fi

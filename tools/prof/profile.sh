@@ -1,6 +1,6 @@
 #!/bin/bash
 # Profile one bench.py kernel with rocprofv3 on the GPU box.
-#   tools/prof/profile.sh TAG WORKLOAD [OP]
+#   tools/prof/profile.sh TAG WORKLOAD [OP [short]]
 # Writes gpurun_out/prof_TAG_WORKLOAD[_OP]/: a kernel-trace --stats pass
 # (timing, with a bench line of its own) and separate PMC passes (one counter
 # group each, never combined with tracing), plus a FETCH_SIZE pass over
@@ -10,11 +10,15 @@ set -u
 TAG=${1:-run}
 WL=${2:-mtu1500}
 OP=${3:-crc32}
+SHORT=${4:-}   # "short": the staged lane-stream entry (bench.py --short-frames)
 SUF=$WL; [ "$OP" != crc32 ] && SUF=${WL}_$OP
+XA=""; [ "$SHORT" = short ] && { SUF=${SUF}_short; XA="--short-frames"; }
 OUT=gpurun_out/prof_${TAG}_${SUF}
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --workload $WL --op $OP --no-cpu-baseline"
+# --no-slice16m: the N=1 mtu1500 line's 16 M-frame sub-measurement would land
+# in the trace and the counter passes as launches of the same kernel
+B="bench.py --workload $WL --op $OP --no-cpu-baseline --no-slice16m $XA"
 BT="$B --prewarm-s 0.5"
 B="$B --prewarm-s 0"
 echo "[prof] kernel trace"
