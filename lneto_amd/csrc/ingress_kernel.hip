@@ -99,7 +99,9 @@ __device__ __forceinline__ uint16_t ing_sum16(uint32_t sum) {  // crc.go:17-21
 template <bool GEN>
 using IngBytes = std::conditional_t<GEN, uint8_t, const uint8_t>;
 
-template <int UNR, bool QW, bool GEN = false>
+// FILT = false: the instance for batches without a stack filter (the filter
+// checks compiled out; the r3 code path and its speed)
+template <int UNR, bool QW, bool GEN = false, bool FILT = true>
 __global__ void __launch_bounds__(kIngBlock)
 ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                       uint32_t flags, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
@@ -260,7 +262,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
       } else {
         const uint32_t et = be(H0, 0);
         bool eth_drop = false, et_handler = true;
-        if (filt.on) {
+        if (FILT && filt.on) {
           // StackEthernet.Demux (internet/stack-ethernet.go:146-152), before
           // ValidateSize: a frame neither broadcast nor for the stack's MAC is
           // dropped unless multicast frames are accepted and the group bit is set
@@ -289,7 +291,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
             v = kErrTruncatedFrame;
           } else {
             const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
-            if (filt.on && filt.ip4 != 0u) {
+            if (FILT && filt.on && filt.ip4 != 0u) {
               // demux4's destination check (internet/stack-ip4.go:108-119), before ValidateExceptCRC
               const uint32_t dst = field32(30);
               const bool mc = (dst & 0xF0u) == 0xE0u, bc = dst == 0xFFFFFFFFu;  // ipv4/definitions.go:17-36
@@ -304,7 +306,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
             if (v == 0) {
               hdr_sum = true;
               const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
-              if (filt.on && !proto_bit(filt.p4, proto)) {
+              if (FILT && filt.on && !proto_bit(filt.p4, proto)) {
                 v_udp4 = kErrPacketDrop;  // nodeByProto nil (stack-ip4.go:135-141), after the header sum
               } else if (proto == 6) {
                 l4_sum = true;
@@ -344,7 +346,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
             v = kErrTruncatedFrame;
           } else {
             const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
-            if (filt.on && (filt.ip6[0] | filt.ip6[1] | filt.ip6[2] | filt.ip6[3]) != 0u) {
+            if (FILT && filt.on && (filt.ip6[0] | filt.ip6[1] | filt.ip6[2] | filt.ip6[3]) != 0u) {
               // demux6's destination check (internet/stack-ip6.go:93-98), before ValidateSize
               const uint32_t d0 = field32(38), d1 = field32(42), d2 = field32(46), d3 = field32(50);
               const bool mine = d0 == filt.ip6[0] && d1 == filt.ip6[1] && d2 == filt.ip6[2] && d3 == filt.ip6[3];
@@ -353,7 +355,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
             if (v != 0) {
             } else if (pl + 40 > M) {
               v = kErrInvalidLengthField;
-            } else if (filt.on && !proto_bit(filt.p6, proto)) {
+            } else if (FILT && filt.on && !proto_bit(filt.p6, proto)) {
               v = kErrPacketDrop;  // nodeByProto nil (stack-ip6.go:107-111), before the sums
             } else if (proto == 6 || proto == 17 || (proto == 58 && (flags & kVerifyIcmp))) {
               // demux6 size-checks the UDP header only; TCP goes straight to the
@@ -573,8 +575,12 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   const uint64_t cap = (uint64_t)num_cus * 128;
   if (grid > cap) grid = cap;
 #endif
+  if (filt.on)
     hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true>), dim3((unsigned)grid), dim3(kIngBlock), 0, stream,
                        bytes, off, n, flags, verdict, seg_len, trim, filt);
+  else
+    hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, false, false>), dim3((unsigned)grid),
+                       dim3(kIngBlock), 0, stream, bytes, off, n, flags, verdict, seg_len, trim, filt);
   return hipGetLastError();
 }
 

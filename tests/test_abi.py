@@ -114,7 +114,8 @@ def test_product_library_holds_only_product_kernels():
         assert re.search(r"ELi0EEEvPKh", k), k              # STR = 0
     others = sorted(re.sub(r"^_ZN3lnx\d+(\w+?kernel).*$", r"\1", k) for k in ks if k not in rows)
     assert others == ["crc32_search_o_kernel", "crc32_stage_kernel", "crc32_stage_kernel", "ingress_verify_kernel",
-                      "ingress_verify_kernel", "ring_segments_kernel", "sum16_lines_kernel"], others
+                      "ingress_verify_kernel", "ingress_verify_kernel", "ring_segments_kernel",
+                      "sum16_lines_kernel"], others  # ingress: filtered / unfiltered verdicts, TX generate
     stage = [k for k in ks if "crc32_stage_kernel" in k]
     assert all(re.search(r"StageModeE\dELi8ELi8E", k) for k in stage), stage  # the product fold / wave count
     research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
