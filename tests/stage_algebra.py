@@ -1,4 +1,4 @@
-"""CPU restatement of the staged lane-stream CRC-32 schedule (crc32_stage.hip;
+"""CPU restatement of the staged lane-stream CRC-32 schedule (stage_kernel.hip;
 DESIGN.md §3.9).  Test infrastructure: it checks the algebra the kernel uses,
 on the host, against zlib (= Go hash/crc32 IEEE, the arithmetic of
 ethernet.CRC32, lneto ethernet/crc.go:19-21).

@@ -1,5 +1,5 @@
 """The staged lane-stream schedule (tests/stage_algebra.py, the restatement of
-crc32_stage.hip) against zlib on the host: resets by select, the ending
+stage_kernel.hip) against zlib on the host: resets by select, the ending
 frame's Z_c, the byte-by-byte half for short and empty frames, and the carry
 of frames that cross stretches (also frames longer than a stretch)."""
 import random
