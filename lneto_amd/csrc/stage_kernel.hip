@@ -49,14 +49,17 @@ constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, h
 // image in HBM (only the carries use them, once per stretch), which frees the
 // room for two more waves' transposes and lists.
 constexpr uint32_t kSTab = 0;  // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
-template <int W, uint32_t BF = kStageBF>
+template <int W, uint32_t BF = kStageBF, bool DEFER = false>
 struct StageLds {
   static_assert((BF + 2) % 64 == 0, "whole-wave list loads");
   static constexpr uint32_t kList = (BF + 2) * 4;      // boundary list bytes per wave (bf + 1 entries + sentinel)
   static constexpr uint32_t kTr = 65536;               // transposes: 8 KiB per wave
   static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists
-  static constexpr bool kNibInLds = kBnd + W * kList + 31 * 512 + 16 <= 163840;
-  static constexpr uint32_t kNib = kBnd + W * kList;   // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
+  // DEFER (variants 312 / 313): Z_16, Z_32, Z_64 byte tables (one shared copy, 12 KiB) after the lists
+  static constexpr uint32_t kZx = kBnd + W * kList;
+  static constexpr uint32_t kZxBytes = DEFER ? 3 * 4096 : 0;
+  static constexpr bool kNibInLds = !DEFER && kBnd + W * kList + 31 * 512 + 16 <= 163840;
+  static constexpr uint32_t kNib = kZx + kZxBytes;     // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
   static constexpr uint32_t kCtr = kNib + (kNibInLds ? 31 * 512 : 0);  // the workgroup's block counter
   static constexpr uint32_t kBytes = kCtr + 16;
   static_assert(kBytes <= 163840, "stage LDS");
@@ -68,6 +71,8 @@ constexpr uint32_t kStageZ4Img = 512 + 31 * 128;
 // then (FOLD 8) the eight slicing-by-8 byte tables T8_k[e] = Z_{8-k}(e), table
 // k entry e at kStageZ8Img + 256 k + e
 constexpr uint32_t kStageZ8Img = kStageZ4Img + 1024;
+// then (DEFER) Z_16, Z_32, Z_64 as four byte tables each: (t, k, e) at kStageZxImg + 1024 t + 256 k + e
+constexpr uint32_t kStageZxImg = kStageZ8Img + 2048;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -186,11 +191,12 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF>
+template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF, bool DEFER = false>
 __global__ void __launch_bounds__(W * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
-  using LY = StageLds<W, BF>;
+  using LY = StageLds<W, BF, DEFER>;
+  static_assert(!DEFER || FOLD == 8, "the deferred correction runs on the slicing-by-8 fold");
   constexpr uint32_t kLast = BF + 1;  // the list's last entry (a sentinel past bf)
   constexpr uint32_t kThreads = W * 64;
   __shared__ __attribute__((aligned(16))) char lds[LY::kBytes];
@@ -227,6 +233,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     if constexpr (LY::kNibInLds)
       for (uint32_t i = t; i < 31u * 128u; i += kThreads)
         reinterpret_cast<uint32_t*>(lds + LY::kNib)[i] = image[512 + i];
+    if constexpr (DEFER)
+      for (uint32_t i = t; i < 3u * 1024u; i += kThreads)
+        reinterpret_cast<uint32_t*>(lds + LY::kZx)[i] = image[kStageZxImg + i];
     if (t == 0) *reinterpret_cast<uint32_t*>(lds + LY::kCtr) = 0;
   }
   __syncthreads();
@@ -453,7 +462,44 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
         const uint32_t lm = in ? (uint32_t)((1ull << (8u * c)) - 1ull) : 0u;
         const uint32_t Kc = c == 0u ? 0xFFFFFFFFu : c == 1u ? kK1 : c == 2u ? kK2 : kK3;
         uint32_t ecap = 0;
-        if constexpr (FOLD == 8) {
+        if constexpr (DEFER) {
+          // no boundary selects in the fold: the plain fold, one capture of r
+          // per 8-byte unit, and the boundary's effect added after the half
+          // (r_true = r_plain ^ Z_{64 - 4d}(e ^ K_c))
+          uint32_t rc = 0;
+          const uint32_t ub = kb >> 1;
+#pragma unroll
+          for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
+            rc = ub == u ? r : rc;
+            r = s_z8half(lds, r ^ w0, z8, 0) ^ s_z8half(lds, w1, z8, 1);
+          }
+          if (__builtin_amdgcn_ballot_w64(in) != 0) {
+            // the boundary unit's two words, from the staged line
+            const uint32_t u = (kb >> 1) & 7u;
+            const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (u >> 1) + rot) & 7u) +
+                                                             8u * (u & 1u));
+            const bool odd = kb & 1u;
+            const uint32_t z4 = s_z8half(lds, rc ^ wp.x, z8, 1);  // the state before w1
+            const uint32_t rd = odd ? z4 : rc;
+            ecap = rd ^ ((odd ? wp.y : wp.x) & lm);
+            // Z_{4m}(ecap ^ K_c), m = 16 - kb dwords, by binary powers: Z_4, Z_8
+            // (the fold's tables), Z_16 / Z_32 / Z_64 (the shared tables)
+            const uint32_t m = 16u - (kb & 15u);
+            uint32_t z = ecap ^ Kc;
+            z = (m & 1u) ? s_z8half(lds, z, z8, 1) : z;
+            z = (m & 2u) ? s_z8half(lds, z, z8, 0) : z;
+#pragma unroll
+            for (uint32_t t = 0; t < 3; ++t) {
+              const uint32_t* zt = reinterpret_cast<const uint32_t*>(lds + LY::kZx) + 1024u * t;
+              const uint32_t zz = __builtin_amdgcn_bitop3_b32(zt[z & 0xFFu], zt[256u + ((z >> 8) & 0xFFu)],
+                                                              zt[512u + ((z >> 16) & 0xFFu)], 0x96) ^
+                                  zt[768u + (z >> 24)];
+              z = (m & (4u << t)) ? zz : z;
+            }
+            r = in ? r ^ z : r;
+          }
+        } else if constexpr (FOLD == 8) {
           // 8-byte units; the unit holding the boundary captures (r, w0, w1)
           uint32_t rc = 0, w0c = 0, w1c = 0;
 #pragma unroll
@@ -585,7 +631,10 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   // and no longer fit its registers once the whole line is read at once)
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (fold == 8) {
+  if (fold == 9) {  // the slicing-by-8 fold with the deferred boundary correction
+    if (big_blocks) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, true); else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, true);
+  } else if (fold == 8) {
     if (big_blocks) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 8, 8); else LNX_STAGE(StageMode::kCrc, 8, 8);
   } else if (big_blocks) {

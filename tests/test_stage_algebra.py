@@ -111,3 +111,27 @@ def test_slicing_by_8_unit_algebra():
             for i in range(c):
                 zc ^= T8[8 - c + i][(e >> (8 * i)) & 0xFF]
             assert zc == S.zc(c, e)
+
+
+def test_deferred_boundary_correction():
+    """Variants 312 / 313: a 64-byte half folded with no boundary select ends
+    at r_plain; with a frame starting at byte c of dword d the true end state
+    is r_plain ^ Z_{64-4d}(e ^ K_c), e = r_d ^ (w_d & lomask(c)) the ending
+    frame's pre-Z_c state (r_d: the state before dword d)."""
+    rng = random.Random(312)
+    for _ in range(2000):
+        r0 = rng.getrandbits(32)
+        w = [rng.getrandbits(32) for _ in range(16)]
+        d, c = rng.randrange(16), rng.randrange(4)
+        lm = (1 << (8 * c)) - 1
+        r, rd = r0, None
+        for i in range(16):
+            if i == d:
+                rd = r
+            r = S.z4(r ^ w[i])
+        plain = r
+        e = rd ^ (w[d] & lm)
+        r = r0
+        for i in range(16):
+            r = S.z4(((w[i] & ~lm & S.MASK) ^ S.K[c]) if i == d else (r ^ w[i]))
+        assert r == plain ^ S.zpow(64 - 4 * d, e ^ S.K[c])
