@@ -617,8 +617,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": ({"crc32": "lnx::crc32_stage_kernel<kCrc, 8, 8>",
-                        "fcs_verify": "lnx::crc32_stage_kernel<kVerify, 8, 8>"} if args.short_frames else {}).get(
+            "kernel": ({"crc32": "lnx::crc32_stage_kernel<kCrc, 8, 8, 382, false, 1>",
+                        "fcs_verify": "lnx::crc32_stage_kernel<kVerify, 8, 8, 382, false, 1>"} if args.short_frames else {}).get(
                 args.op) or {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
                        "search": "lnx::crc32_search_o_kernel",

@@ -123,7 +123,7 @@ std::vector<uint32_t> build_lanes_image() {
 // tables A[e] = Z_2(e), B[e] = Z_1(e), then Z_{2^m} as eight nibble tables
 // for m = 0..30, entry (m, i, v) at dword 512 + 128 m + 16 i + v.
 std::vector<uint32_t> build_stage_image() {
-  std::vector<uint32_t> t(512 + 31 * 128 + 1024 + 2048 + 3 * 1024);
+  std::vector<uint32_t> t(512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 4 * 1024);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 2), t[256 + e] = zshift_bytes(e, 1);
   for (uint32_t m = 0; m < 31; ++m)
     for (uint32_t i = 0; i < 8; ++i)
@@ -136,6 +136,10 @@ std::vector<uint32_t> build_stage_image() {
     for (uint32_t k = 0; k < 4; ++k)
       for (uint32_t e = 0; e < 256; ++e)
         t[512 + 31 * 128 + 1024 + 2048 + 1024 * z + 256 * k + e] = zshift_bytes(e << (8 * k), 16 << z);
+  for (uint32_t z = 0; z < 4; ++z)  // Z_8, Z_16, Z_24, Z_32 byte tables (two chains per half)
+    for (uint32_t k = 0; k < 4; ++k)
+      for (uint32_t e = 0; e < 256; ++e)
+        t[512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 1024 * z + 256 * k + e] = zshift_bytes(e << (8 * k), 8 * (z + 1));
   return t;
 }
 
@@ -574,10 +578,12 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   // slicing-by-2 fold; 302 / 303: the same with the 16-column Z_4 fold;
   // 304-307: 300-303 with 10 waves per workgroup instead of 8 (retired);
   // 308 / 309: 302 / 303 with 766-frame blocks; 310 / 311: the slicing-by-8 fold;
-  // 312 / 313: the slicing-by-8 fold with the boundary correction deferred
-  hipError_t e = var >= 300 && var <= 313
+  // 312 / 313: the slicing-by-8 fold with the boundary correction deferred;
+  // 314 / 315: the slicing-by-8 fold with the boundary word patched per half;
+  // 316 / 317: 314 / 315 with each half folded as two chains of four units
+  hipError_t e = var >= 300 && var <= 317
                      ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1,
-                                          var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
+                                          var >= 316 ? 11 : var >= 314 ? 10 : var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
                                           var >= 304 && var < 308 ? 10 : 8, c->d_stage, c->num_cus,
                                           static_cast<hipStream_t>(stream), var == 308 || var == 309)
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,

@@ -49,16 +49,19 @@ constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, h
 // image in HBM (only the carries use them, once per stretch), which frees the
 // room for two more waves' transposes and lists.
 constexpr uint32_t kSTab = 0;  // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
-template <int W, uint32_t BF = kStageBF, bool DEFER = false>
+template <int W, uint32_t BF = kStageBF, uint32_t ZXB = 0>
 struct StageLds {
   static_assert((BF + 2) % 64 == 0, "whole-wave list loads");
   static constexpr uint32_t kList = (BF + 2) * 4;      // boundary list bytes per wave (bf + 1 entries + sentinel)
   static constexpr uint32_t kTr = 65536;               // transposes: 8 KiB per wave
   static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists
-  // DEFER (variants 312 / 313): Z_16, Z_32, Z_64 byte tables (one shared copy, 12 KiB) after the lists
+  // ZXB bytes of shared single-column byte tables after the lists: Z_16, Z_32,
+  // Z_64 (DEFER, variants 312 / 313, 12 KiB) or Z_8, Z_16, Z_24, Z_32 (two
+  // chains per half, variants 316 / 317, 16 KiB); the nibble tables then
+  // stay in HBM
   static constexpr uint32_t kZx = kBnd + W * kList;
-  static constexpr uint32_t kZxBytes = DEFER ? 3 * 4096 : 0;
-  static constexpr bool kNibInLds = !DEFER && kBnd + W * kList + 31 * 512 + 16 <= 163840;
+  static constexpr uint32_t kZxBytes = ZXB;
+  static constexpr bool kNibInLds = ZXB == 0 && kBnd + W * kList + 31 * 512 + 16 <= 163840;
   static constexpr uint32_t kNib = kZx + kZxBytes;     // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
   static constexpr uint32_t kCtr = kNib + (kNibInLds ? 31 * 512 : 0);  // the workgroup's block counter
   static constexpr uint32_t kBytes = kCtr + 16;
@@ -73,6 +76,8 @@ constexpr uint32_t kStageZ4Img = 512 + 31 * 128;
 constexpr uint32_t kStageZ8Img = kStageZ4Img + 1024;
 // then (DEFER) Z_16, Z_32, Z_64 as four byte tables each: (t, k, e) at kStageZxImg + 1024 t + 256 k + e
 constexpr uint32_t kStageZxImg = kStageZ8Img + 2048;
+// then (two chains per half) Z_8, Z_16, Z_24, Z_32: (t, k, e) at kStageZyImg + 1024 t + 256 k + e = Z_{8(t+1)}(e << 8k)
+constexpr uint32_t kStageZyImg = kStageZxImg + 3072;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -125,6 +130,17 @@ __device__ __forceinline__ uint32_t s_z8half(const char* lds, uint32_t v, const 
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v, z8.base[4 * h + i], z8.sel[i]));
   return __builtin_amdgcn_bitop3_b32(y[0], y[1], y[2], 0x96) ^ y[3];
+}
+// a whole unit: Z_8(v0) ^ Z_4(v1), the eight lookups folded in four ops (the
+// v1 side, off the chain, first)
+__device__ __forceinline__ uint32_t s_z8unit(const char* lds, uint32_t v0, uint32_t v1, const Z8Lane& z8) {
+  uint32_t y[8];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) y[4 + i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v1, z8.base[4 + i], z8.sel[i]));
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v0, z8.base[i], z8.sel[i]));
+  const uint32_t t = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(y[4], y[5], y[6], 0x96), y[7], y[0], 0x96);
+  return __builtin_amdgcn_bitop3_b32(t, y[1], y[2], 0x96) ^ y[3];
 }
 // the FOLD 4 lookups' per-lane v_perm bases / selectors: lookup i reads table
 // k = (i + h) & 3 at byte (v.byte_k << 8) | (k << 6) | (c << 2)
@@ -191,12 +207,13 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF, bool DEFER = false>
+template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF, bool DEFER = false, int PATCH = 0>
 __global__ void __launch_bounds__(W * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
-  using LY = StageLds<W, BF, DEFER>;
+  using LY = StageLds<W, BF, DEFER ? 3u * 4096u : PATCH == 2 ? 4u * 4096u : 0u>;
   static_assert(!DEFER || FOLD == 8, "the deferred correction runs on the slicing-by-8 fold");
+  static_assert(PATCH == 0 || (FOLD == 8 && !DEFER), "the patched boundary word runs on the slicing-by-8 fold");
   constexpr uint32_t kLast = BF + 1;  // the list's last entry (a sentinel past bf)
   constexpr uint32_t kThreads = W * 64;
   __shared__ __attribute__((aligned(16))) char lds[LY::kBytes];
@@ -233,9 +250,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     if constexpr (LY::kNibInLds)
       for (uint32_t i = t; i < 31u * 128u; i += kThreads)
         reinterpret_cast<uint32_t*>(lds + LY::kNib)[i] = image[512 + i];
-    if constexpr (DEFER)
-      for (uint32_t i = t; i < 3u * 1024u; i += kThreads)
-        reinterpret_cast<uint32_t*>(lds + LY::kZx)[i] = image[kStageZxImg + i];
+    if constexpr (LY::kZxBytes != 0)
+      for (uint32_t i = t; i < LY::kZxBytes / 4u; i += kThreads)
+        reinterpret_cast<uint32_t*>(lds + LY::kZx)[i] = image[(DEFER ? kStageZxImg : kStageZyImg) + i];
     if (t == 0) *reinterpret_cast<uint32_t*>(lds + LY::kCtr) = 0;
   }
   __syncthreads();
@@ -499,6 +516,69 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
             }
             r = in ? r ^ z : r;
           }
+        } else if constexpr (PATCH == 2) {
+          // the patched boundary word, and the half as two chains of four
+          // units: A from r, B from 0 (independent: two LDS round trips in
+          // flight per lane); after the half r = Z_32(A) ^ B, or B alone when
+          // the boundary lies in B.  A boundary in B captured B's local state:
+          // the true one adds Z_{8(u-4)}(A), read with Z_32(A) in one round
+          // trip from the shared Z_8 / Z_16 / Z_24 / Z_32 tables
+          const uint32_t ub = (kb >> 1) & 7u;
+          const bool odd = (kb & 1u) != 0u;
+          const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (ub >> 1) + rot) & 7u) +
+                                                           8u * (ub & 1u));
+          const uint32_t wb = __builtin_amdgcn_bitop3_b32(odd ? wp.y : wp.x, lm, Kc, 0x9A);
+          const uint32_t wb0 = odd ? 0u : wb;
+          const uint32_t kbu = kb >> 1;  // (49 in a lane without a boundary)
+          uint32_t ra = r, rbv = 0, rc = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 4; ++u) {
+            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
+            const uint32_t x0 = q[2 + (u >> 1)][(2u * u) & 3u], x1w = q[2 + (u >> 1)][(2u * u + 1u) & 3u];
+            const bool au = kbu == u, a1 = au && odd;
+            const bool bu = kbu == u + 4u, b1 = bu && odd;
+            rc = au ? ra : bu ? rbv : rc;
+            ra = s_z8unit(lds, au ? wb0 : ra ^ w0, a1 ? wb : w1, z8);
+            rbv = s_z8unit(lds, bu ? wb0 : rbv ^ x0, b1 ? wb : x1w, z8);
+          }
+          const bool inb = kbu - 4u < 4u;
+          const uint32_t* zy = reinterpret_cast<const uint32_t*>(lds + LY::kZx);
+          const uint32_t zsel = 1024u * ((kbu - 5u) & 3u);  // Z_{8(u-4)} for u = 5..7
+          uint32_t a32[4], ac[4];
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t e = (ra >> (8u * k)) & 0xFFu;
+            a32[k] = zy[3u * 1024u + 256u * k + e];
+            ac[k] = zy[zsel + 256u * k + e];
+          }
+          const uint32_t z32 = __builtin_amdgcn_bitop3_b32(a32[0], a32[1], a32[2], 0x96) ^ a32[3];
+          const uint32_t zc = __builtin_amdgcn_bitop3_b32(ac[0], ac[1], ac[2], 0x96) ^ ac[3];
+          r = inb ? rbv : z32 ^ rbv;
+          const uint32_t rct = inb ? rc ^ (kbu == 4u ? ra : zc) : rc;
+          const uint32_t z4t = s_z8half(lds, rct ^ wp.x, z8, 1);
+          ecap = odd ? z4t ^ (wp.y & lm) : rct ^ (wp.x & lm);
+        } else if constexpr (PATCH == 1) {
+          // the boundary word patched once per half, read back from the staged
+          // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
+          // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
+          // = 0 drops r), so a unit costs one compare and two selects
+          const uint32_t ub = (kb >> 1) & 7u;
+          const bool odd = (kb & 1u) != 0u;
+          const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (ub >> 1) + rot) & 7u) +
+                                                           8u * (ub & 1u));
+          const uint32_t wb = __builtin_amdgcn_bitop3_b32(odd ? wp.y : wp.x, lm, Kc, 0x9A);
+          const uint32_t wb0 = odd ? 0u : wb;
+          const uint32_t kbu = kb >> 1;  // (49 in a lane without a boundary)
+          uint32_t rc = 0;
+#pragma unroll
+          for (uint32_t u = 0; u < 8; ++u) {
+            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
+            const bool au = kbu == u, a1 = au && odd;
+            rc = au ? r : rc;
+            r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
+          }
+          const uint32_t z4t = s_z8half(lds, rc ^ wp.x, z8, 1);
+          ecap = odd ? z4t ^ (wp.y & lm) : rc ^ (wp.x & lm);
         } else if constexpr (FOLD == 8) {
           // 8-byte units; the unit holding the boundary captures (r, w0, w1)
           uint32_t rc = 0, w0c = 0, w1c = 0;
@@ -631,7 +711,16 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   // and no longer fit its registers once the whole line is read at once)
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (fold == 9) {  // the slicing-by-8 fold with the deferred boundary correction
+  if (fold == 10 || fold == 11) {  // the slicing-by-8 fold with the boundary word patched once per half (11: two chains per half)
+    if (big_blocks) return hipErrorInvalidValue;
+    if (fold == 11) {
+      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 2);
+      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 2);
+    } else {
+      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 1);
+      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 1);
+    }
+  } else if (fold == 9) {  // the slicing-by-8 fold with the deferred boundary correction
     if (big_blocks) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, true); else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, true);
   } else if (fold == 8) {
@@ -646,9 +735,10 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
     if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
   }
 #undef LNX_STAGE_W
-#else  // the product form only: the slicing-by-8 fold, 8 waves, 382-frame blocks
+#else  // the product form only: the slicing-by-8 fold with the patched boundary word, 8 waves, 382-frame blocks
   if (fold != 8 || waves != 8 || big_blocks) return hipErrorInvalidValue;
-  if (verify) LNX_STAGE(StageMode::kVerify, 8, 8); else LNX_STAGE(StageMode::kCrc, 8, 8);
+  if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 1);
+  else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 1);
 #endif
 #undef LNX_STAGE
   return hipGetLastError();

@@ -135,3 +135,97 @@ def test_deferred_boundary_correction():
         for i in range(16):
             r = S.z4(((w[i] & ~lm & S.MASK) ^ S.K[c]) if i == d else (r ^ w[i]))
         assert r == plain ^ S.zpow(64 - 4 * d, e ^ S.K[c])
+
+
+def test_patched_boundary_word_half():
+    """Variants 314 / 315: the boundary word patched once per half, p = (w_kb &
+    ~lm) ^ K_c; unit u = kb >> 1 enters (p, w1) for a boundary in w0 and (0, p)
+    for one in w1 (Z_8(0) = 0 drops r), every other unit (r ^ w0, w1).  The
+    half's end state equals the dword-serial fold with the reset at dword kb,
+    and the ending frame's pre-Z_c state comes from the captured r and the
+    unit's two words re-read from the line."""
+    rng = random.Random(314)
+    T8 = [[S.zc(8 - k, e) for e in range(256)] for k in range(8)]
+
+    def half(v, h):
+        out = 0
+        for k in range(4):
+            out ^= T8[4 * h + k][(v >> (8 * k)) & 0xFF]
+        return out
+
+    for _ in range(2000):
+        r0 = rng.getrandbits(32)
+        w = [rng.getrandbits(32) for _ in range(16)]
+        kb, c = rng.randrange(16), rng.randrange(4)
+        lm = (1 << (8 * c)) - 1
+        odd, ub = kb & 1, kb >> 1
+        p = (w[kb] & ~lm & S.MASK) ^ S.K[c]
+        r, rc = r0, 0
+        for u in range(8):
+            w0, w1 = w[2 * u], w[2 * u + 1]
+            au = u == ub
+            rc = r if au else rc
+            v0 = (0 if odd else p) if au else r ^ w0
+            v1 = p if (au and odd) else w1
+            r = half(v0, 0) ^ half(v1, 1)
+        # the dword-serial fold with the reset at dword kb
+        rs, e_ref = r0, None
+        for i in range(16):
+            if i == kb:
+                e_ref = rs ^ (w[i] & lm)
+                rs = S.z4(p)
+            else:
+                rs = S.z4(rs ^ w[i])
+        assert r == rs
+        wx, wy = w[2 * ub], w[2 * ub + 1]
+        e = (half(rc ^ wx, 1) ^ (wy & lm)) if odd else rc ^ (wx & lm)
+        assert e == e_ref
+
+
+def test_two_chain_half():
+    """Variants 316 / 317: the half as chain A (units 0-3, from r) and chain B
+    (units 4-7, from 0), r = Z_32(A) ^ B, or B alone when the boundary lies in
+    B; a boundary in B captures B's local state, the true one adds
+    Z_{8(u-4)}(A)."""
+    rng = random.Random(316)
+    T8 = [[S.zc(8 - k, e) for e in range(256)] for k in range(8)]
+
+    def half(v, h):
+        out = 0
+        for k in range(4):
+            out ^= T8[4 * h + k][(v >> (8 * k)) & 0xFF]
+        return out
+
+    def unit(r, w0, w1, au, odd, p):
+        v0 = (0 if odd else p) if au else r ^ w0
+        return half(v0, 0) ^ half(p if (au and odd) else w1, 1)
+
+    for _ in range(2000):
+        r0 = rng.getrandbits(32)
+        w = [rng.getrandbits(32) for _ in range(16)]
+        kb, c = rng.randrange(16), rng.randrange(4)
+        lm = (1 << (8 * c)) - 1
+        odd, ub = kb & 1, kb >> 1
+        p = (w[kb] & ~lm & S.MASK) ^ S.K[c]
+        ra, rb, rc = r0, 0, 0
+        for u in range(4):
+            if u == ub:
+                rc = ra
+            elif u + 4 == ub:
+                rc = rb
+            ra = unit(ra, w[2 * u], w[2 * u + 1], u == ub, odd, p)
+            rb = unit(rb, w[8 + 2 * u], w[9 + 2 * u], u + 4 == ub, odd, p)
+        inb = ub >= 4
+        r = rb if inb else S.zpow(32, ra) ^ rb
+        rct = rc ^ S.zpow(8 * (ub - 4), ra) if inb else rc
+        rs, e_ref = r0, None
+        for i in range(16):
+            if i == kb:
+                e_ref = rs ^ (w[i] & lm)
+                rs = S.z4(p)
+            else:
+                rs = S.z4(rs ^ w[i])
+        assert r == rs
+        wx, wy = w[2 * ub], w[2 * ub + 1]
+        e = (half(rct ^ wx, 1) ^ (wy & lm)) if odd else rct ^ (wx & lm)
+        assert e == e_ref
