@@ -44,6 +44,7 @@ enum class StageMode : int { kCrc = 0, kVerify = 1 };
 
 constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
 constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, half the per-block overhead
+constexpr uint32_t kStageBFSmall = 190, kStageBFMid = 254;  // variants 318-321: shorter blocks, a shorter tail
 // LDS layout (bytes) for W waves per workgroup.  W = 8: the Z_{2^m} nibble
 // tables live in LDS too; W = 10 (variants 304-307): they are read from the
 // image in HBM (only the carries use them, once per stretch), which frees the
@@ -272,16 +273,64 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   // this lane's read-back addresses: piece i of its line at rb + 16 ((i + lane) & 7)
   const uint32_t rb = 1024u * (lane & 7u) + 128u * (lane >> 3), rot = lane & 7u;
 
+  auto grab = [&]() -> uint32_t {
+    uint32_t b = 0;
+    if (lane == 0) b = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + LY::kCtr), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+  };
+  // PF (variants 322 / 323): the next block's offsets (its boundary list, A
+  // and E among them) are loaded while this block folds.  The loads are inline
+  // asm, so hipcc neither waits for them early nor counts them; the ring's
+  // vmcnt(0) at the block end (and once before the first block) makes them
+  // ready, and that asm names them as operands, so no use moves above it.
+  // They are older than every ring operation, so the ring's static vmcnt(10)
+  // still covers its slot.
+  constexpr bool PF = PATCH == 3;
+  constexpr uint32_t kNL = (BF + 2) / 64;
+  static_assert(!PF || kNL == 6, "the prefetch asm names six offsets per lane");
+  uint64_t pre[6] = {0, 0, 0, 0, 0, 0};
+  auto prefetch = [&](uint32_t b) {
+    const uint64_t fr = (uint64_t)b * BF;
+    const uint32_t bfx = fr < nslice ? (uint32_t)(nslice - fr < BF ? nslice - fr : BF) : 0u;
+    const uint64_t* p0 = off + fb0 + (fr < nslice ? fr : 0u);  // (past the slice: entry fb0, a valid address)
+#pragma unroll
+    for (uint32_t i = 0; i < 6; ++i) {
+      const uint32_t jj = lane + 64u * i;
+      const uint64_t* p = p0 + (jj <= bfx ? jj : bfx);
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=&v"(pre[i]) : "v"(p));
+    }
+  };
+  auto pre_ready = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(pre[0]), "+v"(pre[1]), "+v"(pre[2]), "+v"(pre[3]), "+v"(pre[4]), "+v"(pre[5]));
+  };
+  uint32_t blk_pf = 0;
+  if constexpr (PF) {
+    blk_pf = grab();
+    prefetch(blk_pf);
+    pre_ready();
+  }
+
   for (;;) {
-    uint32_t blk = 0;
-    if (lane == 0) blk = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + LY::kCtr), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-    blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk);
+    const uint32_t blk = PF ? blk_pf : grab();
     const uint64_t f0r = (uint64_t)blk * BF;  // relative to fb0
     if (f0r >= nslice) break;
     const uint32_t bf = (uint32_t)(nslice - f0r < BF ? nslice - f0r : BF);
     const uint64_t f0 = fb0 + f0r;
-    const uint64_t A = off[f0], E = off[f0 + bf];
+    uint64_t A, E;
+    if constexpr (PF) {
+      uint64_t ev = pre[0];
+#pragma unroll
+      for (uint32_t i = 1; i < 6; ++i) ev = (bf >> 6) == i ? pre[i] : ev;
+      const uint32_t el = bf & 63u;
+      A = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pre[0], 0) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pre[0] >> 32), 0) << 32);
+      E = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ev, (int)el) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ev >> 32), (int)el) << 32);
+    } else {
+      A = off[f0], E = off[f0 + bf];
+    }
     const uint8_t* pa = bytes + A;
     const uint32_t adj = (uint32_t)(reinterpret_cast<uintptr_t>(pa) & 127u);
     const uint64_t span = E > A ? E - A + adj : adj;
@@ -289,9 +338,13 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 #pragma unroll
     for (uint32_t i = 0; i < (BF + 2) / 64; ++i) {  // (whole-wave loads: entry j > bf re-reads entry bf)
       const uint32_t j = lane + 64u * i;
-      const uint64_t o = off[f0 + (j <= bf ? j : bf)];
+      const uint64_t o = PF ? pre[i] : off[f0 + (j <= bf ? j : bf)];
       const uint32_t x = o > A ? (uint32_t)(o - A) + adj : adj;  // (non-decreasing offsets: o >= A)
       list[j] = j <= bf ? x : kSNone;
+    }
+    if constexpr (PF) {
+      blk_pf = grab();
+      prefetch(blk_pf);
     }
     __builtin_amdgcn_wave_barrier();
     if (span >= (1ull << 31) - 65536) {
@@ -320,6 +373,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, (uint32_t)(f0r + j), 0, 0);
         }
       }
+      if constexpr (PF) pre_ready();
       continue;
     }
     const uint32_t sp = (uint32_t)span;
@@ -333,27 +387,6 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     // so the piece holding E's last byte never crosses a page)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pa - adj), (short)0,
                                                                         (int)((sp + 15u) & ~15u), 0x00020000);
-    // ---- this lane's stretch [Sk, Sk + Q) and its first boundary j = lower_bound(list, Sk)
-    const uint32_t Sk = lane * Q;
-    uint32_t lo = 0, hi = bf + 1u;
-    while (__builtin_amdgcn_ballot_w64(lo < hi) != 0) {
-      const uint32_t mid = (lo + hi) >> 1;
-      const uint32_t xm = list[mid < kLast ? mid : kLast];
-      if (lo < hi) {
-        if (xm >= Sk) hi = mid; else lo = mid + 1u;
-      }
-    }
-    const uint32_t jstart = lo;
-    uint32_t j = lo;
-    // the lane's next three boundaries: x (due), x1 (the slow-half test), x2
-    // (read one advance ahead, so that an advance never waits for the list)
-    uint32_t x = list[j], x1 = list[j + 1u < kLast ? j + 1u : kLast];  // (j = bf + 1 past the block end)
-    uint32_t x2 = list[j + 2u < kLast ? j + 2u : kLast];
-    uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
-    uint32_t r = 0;
-    bool first = true;
-    uint32_t rec_j = 0, rec_S = 0, rec_d = 0;  // the first boundary's frame (carry pending)
-    bool rec = false;
     // load offsets: instruction m reads stretch s = 8 (lane >> 3) + m, piece ((lane & 7) - s) & 7
     uint32_t lo_m[8];
 #pragma unroll
@@ -403,6 +436,33 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
                      ::"v"(hv0), "v"(hf0), "v"(hv1), "v"(hf1), "s"(out_rsrc) : "memory");
       hf0 = hf1 = kSOOB;
     };
+    // the block's first two rounds go out before the boundary search
+    u32x4 buf0[8], buf1[8];
+    flush();  // (two stores, so that the first waits count alike)
+    issue(buf0, 0);
+    flush();
+    issue(buf1, 1);
+    // ---- this lane's stretch [Sk, Sk + Q) and its first boundary j = lower_bound(list, Sk)
+    const uint32_t Sk = lane * Q;
+    uint32_t lo = 0, hi = bf + 1u;
+    while (__builtin_amdgcn_ballot_w64(lo < hi) != 0) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint32_t xm = list[mid < kLast ? mid : kLast];
+      if (lo < hi) {
+        if (xm >= Sk) hi = mid; else lo = mid + 1u;
+      }
+    }
+    const uint32_t jstart = lo;
+    uint32_t j = lo;
+    // the lane's next three boundaries: x (due), x1 (the slow-half test), x2
+    // (read one advance ahead, so that an advance never waits for the list)
+    uint32_t x = list[j], x1 = list[j + 1u < kLast ? j + 1u : kLast];  // (j = bf + 1 past the block end)
+    uint32_t x2 = list[j + 2u < kLast ? j + 2u : kLast];
+    uint32_t xprev = j > 0 ? list[j - 1u] : 0u;
+    uint32_t r = 0;
+    bool first = true;
+    uint32_t rec_j = 0, rec_S = 0, rec_d = 0;  // the first boundary's frame (carry pending)
+    bool rec = false;
     // the end of the frame at boundary j (state S, at position xe): a result,
     // or the stretch's first frame, held until the carries are known; the
     // result goes to the half's hold (slot h) or, in a byte-serial half, out at once
@@ -557,7 +617,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           const uint32_t rct = inb ? rc ^ (kbu == 4u ? ra : zc) : rc;
           const uint32_t z4t = s_z8half(lds, rct ^ wp.x, z8, 1);
           ecap = odd ? z4t ^ (wp.y & lm) : rct ^ (wp.x & lm);
-        } else if constexpr (PATCH == 1) {
+        } else if constexpr (PATCH == 1 || PATCH == 3) {
           // the boundary word patched once per half, read back from the staged
           // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
           // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
@@ -641,11 +701,6 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
         }
       }
     };
-    u32x4 buf0[8], buf1[8];
-    flush();  // (two stores, so that the first waits count alike)
-    issue(buf0, 0);
-    flush();
-    issue(buf1, 1);
     for (uint32_t rr = 0; rr < rounds; rr += 2) {
       round_step(buf0, rr);
       if (rr + 1u < rounds) round_step(buf1, rr + 1u);
@@ -653,6 +708,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     flush();
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(buf0[0]), "+v"(buf0[1]), "+v"(buf0[2]), "+v"(buf0[3]), "+v"(buf0[4]),
                  "+v"(buf0[5]), "+v"(buf0[6]), "+v"(buf0[7]));
+    if constexpr (PF) asm volatile("" : "+v"(pre[0]), "+v"(pre[1]), "+v"(pre[2]), "+v"(pre[3]), "+v"(pre[4]), "+v"(pre[5]));
     asm volatile("" : "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]), "+v"(buf1[4]), "+v"(buf1[5]),
                  "+v"(buf1[6]), "+v"(buf1[7]));
     // ---- carries: the true register at each stretch's start
@@ -698,7 +754,7 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
                               int fold, int waves, const void* image, int num_cus, hipStream_t stream,
                               bool big_blocks) {
   if (n == 0) return hipSuccess;
-  const uint64_t bfl = big_blocks ? kStageBFBig : kStageBF;
+  const uint64_t bfl = big_blocks ? kStageBFBig : fold == 12 ? kStageBFSmall : fold == 13 ? kStageBFMid : kStageBF;
   uint64_t grid = (n + bfl - 1) / bfl;
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const uint64_t per = (n + grid - 1) / grid;
@@ -711,7 +767,20 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   // and no longer fit its registers once the whole line is read at once)
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (fold == 10 || fold == 11) {  // the slicing-by-8 fold with the boundary word patched once per half (11: two chains per half)
+  if (fold == 14) {  // the product form with the next block's offsets loaded ahead
+    if (big_blocks) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 3);
+    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 3);
+  } else if (fold == 12 || fold == 13) {  // the product form (patched boundary word) with 190- / 254-frame blocks
+    if (big_blocks) return hipErrorInvalidValue;
+    if (fold == 12) {
+      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBFSmall, false, 1);
+      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBFSmall, false, 1);
+    } else {
+      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBFMid, false, 1);
+      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBFMid, false, 1);
+    }
+  } else if (fold == 10 || fold == 11) {  // the slicing-by-8 fold with the boundary word patched once per half (11: two chains per half)
     if (big_blocks) return hipErrorInvalidValue;
     if (fold == 11) {
       if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 2);
