@@ -45,6 +45,7 @@ enum class StageMode : int { kCrc = 0, kVerify = 1 };
 constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
 constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, half the per-block overhead
 constexpr uint32_t kStageBFSmall = 190, kStageBFMid = 254;  // variants 318-321: shorter blocks, a shorter tail
+constexpr uint32_t kStageBF510 = 510;  // variants 324 / 325: the longest lists that leave the nibble tables in LDS
 // LDS layout (bytes) for W waves per workgroup.  W = 8: the Z_{2^m} nibble
 // tables live in LDS too; W = 10 (variants 304-307): they are read from the
 // image in HBM (only the carries use them, once per stretch), which frees the
@@ -754,7 +755,8 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
                               int fold, int waves, const void* image, int num_cus, hipStream_t stream,
                               bool big_blocks) {
   if (n == 0) return hipSuccess;
-  const uint64_t bfl = big_blocks ? kStageBFBig : fold == 12 ? kStageBFSmall : fold == 13 ? kStageBFMid : kStageBF;
+  const uint64_t bfl = big_blocks ? kStageBFBig : fold == 12 ? kStageBFSmall : fold == 13 ? kStageBFMid
+                                                                            : fold == 15 ? kStageBF510 : kStageBF;
   uint64_t grid = (n + bfl - 1) / bfl;
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const uint64_t per = (n + grid - 1) / grid;
@@ -767,7 +769,11 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   // and no longer fit its registers once the whole line is read at once)
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (fold == 14) {  // the product form with the next block's offsets loaded ahead
+  if (fold == 15) {  // the product form with 510-frame blocks
+    if (big_blocks) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF510, false, 1);
+    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF510, false, 1);
+  } else if (fold == 14) {  // the product form with the next block's offsets loaded ahead
     if (big_blocks) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 3);
     else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 3);
