@@ -767,6 +767,12 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
 #ifdef LNX_RESEARCH  // variants 300-303, 308, 309: both folds, 382- or 766-frame blocks
   // (10 waves per workgroup, variants 304-307, measured no faster in round 4
   // and no longer fit its registers once the whole line is read at once)
+  if (fold == 16) {  // the product form with 6 waves (1.5 per SIMD): how much the second wave per SIMD buys
+    if (big_blocks) return hipErrorInvalidValue;
+    if (verify) LNX_STAGE(StageMode::kVerify, 8, 6, kStageBF, false, 1);
+    else LNX_STAGE(StageMode::kCrc, 8, 6, kStageBF, false, 1);
+    return hipGetLastError();
+  }
   if (waves != 8) return hipErrorInvalidValue;
 #define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
   if (fold == 15) {  // the product form with 510-frame blocks

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 
-CRC_VARS = [300, 302, 308, 310, 312, 314, 316, 318, 320, 322, 324]  # slicing-by-2 / 16-column Z_4 / slicing-by-8 fold, 766-frame blocks, deferred correction, patched boundary word, two chains per half, 190- / 254-frame blocks, offsets a block ahead, 510-frame blocks
+CRC_VARS = [300, 302, 308, 310, 312, 314, 316, 318, 320, 322, 324, 326]  # slicing-by-2 / 16-column Z_4 / slicing-by-8 fold, 766-frame blocks, deferred correction, patched boundary word, two chains per half, 190- / 254-frame blocks, offsets a block ahead, 510-frame blocks, 6 waves
 
 
 def _lib():
@@ -107,7 +107,7 @@ def test_gpu_stage_small_batches(cuda, var):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", [301, 303, 309, 311, 313, 315, 317, 319, 321, 323, 325])
+@pytest.mark.parametrize("var", [301, 303, 309, 311, 313, 315, 317, 319, 321, 323, 325, 327])
 def test_gpu_stage_verify(cuda, var):
     """Variant 301: FCS verify (residue) over frames carrying their LE FCS;
     a third get one flipped byte; runts under 4 bytes fail."""
