@@ -503,8 +503,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       asm volatile("s_waitcnt vmcnt(10)"
                    : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
                      "+v"(cur[6]), "+v"(cur[7]));
+      if constexpr (PATCH != 4)  // (variant 328, timing only: the lines read back stale)
 #pragma unroll
-      for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
+        for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
       flush();
       issue(cur, rr + 2u);
       // the lane's whole line in one LDS round trip (both halves)
@@ -618,7 +619,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           const uint32_t rct = inb ? rc ^ (kbu == 4u ? ra : zc) : rc;
           const uint32_t z4t = s_z8half(lds, rct ^ wp.x, z8, 1);
           ecap = odd ? z4t ^ (wp.y & lm) : rct ^ (wp.x & lm);
-        } else if constexpr (PATCH == 1 || PATCH == 3) {
+        } else if constexpr (PATCH == 1 || PATCH == 3 || PATCH == 4 || PATCH == 5) {
           // the boundary word patched once per half, read back from the staged
           // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
           // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
@@ -636,7 +637,10 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
             const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
             const bool au = kbu == u, a1 = au && odd;
             rc = au ? r : rc;
-            r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
+            if constexpr (PATCH == 5)  // (variant 330, timing only: a two-op stand-in for the unit's lookups)
+              r = __builtin_amdgcn_alignbit(au ? wb0 : r ^ w0, a1 ? wb : w1, 7) ^ (a1 ? wb : w1);
+            else
+              r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
           }
           const uint32_t z4t = s_z8half(lds, rc ^ wp.x, z8, 1);
           ecap = odd ? z4t ^ (wp.y & lm) : rc ^ (wp.x & lm);
@@ -767,6 +771,11 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
 #ifdef LNX_RESEARCH  // variants 300-303, 308, 309: both folds, 382- or 766-frame blocks
   // (10 waves per workgroup, variants 304-307, measured no faster in round 4
   // and no longer fit its registers once the whole line is read at once)
+  if (fold == 17 || fold == 18) {  // timing-only diagnostics of the product form (wrong results)
+    if (fold == 17) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 4);
+    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 5);
+    return hipGetLastError();
+  }
   if (fold == 16) {  // the product form with 6 waves (1.5 per SIMD): how much the second wave per SIMD buys
     if (big_blocks) return hipErrorInvalidValue;
     if (verify) LNX_STAGE(StageMode::kVerify, 8, 6, kStageBF, false, 1);
