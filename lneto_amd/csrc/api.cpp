@@ -585,10 +585,11 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   // 322 / 323: 314 / 315 with the next block's offsets loaded ahead;
   // 324 / 325: 314 / 315 with 510-frame blocks; 326 / 327: 314 / 315 with 6 waves;
   // 328 / 330: timing only (wrong results): 314 without the transpose writes,
-  // 314 with a two-op stand-in for the lookups
-  hipError_t e = (var >= 300 && var <= 327) || var == 328 || var == 330
+  // 314 with a two-op stand-in for the lookups; 332: 314 without the ending
+  // frames' capture and Z_c; 334: 314 without the carries
+  hipError_t e = (var >= 300 && var <= 327) || var == 328 || var == 330 || var == 332 || var == 334
                      ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1,
-                                          var == 330 ? 18 : var == 328 ? 17 : var >= 326 ? 16 : var >= 324 ? 15 : var >= 322 ? 14 : var >= 320 ? 13 : var >= 318 ? 12 : var >= 316 ? 11 : var >= 314 ? 10 : var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
+                                          var == 334 ? 20 : var == 332 ? 19 : var == 330 ? 18 : var == 328 ? 17 : var >= 326 ? 16 : var >= 324 ? 15 : var >= 322 ? 14 : var >= 320 ? 13 : var >= 318 ? 12 : var >= 316 ? 11 : var >= 314 ? 10 : var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
                                           var >= 304 && var < 308 ? 10 : 8, c->d_stage, c->num_cus,
                                           static_cast<hipStream_t>(stream), var == 308 || var == 309)
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,

@@ -619,7 +619,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
           const uint32_t rct = inb ? rc ^ (kbu == 4u ? ra : zc) : rc;
           const uint32_t z4t = s_z8half(lds, rct ^ wp.x, z8, 1);
           ecap = odd ? z4t ^ (wp.y & lm) : rct ^ (wp.x & lm);
-        } else if constexpr (PATCH == 1 || PATCH == 3 || PATCH == 4 || PATCH == 5) {
+        } else if constexpr (PATCH == 1 || PATCH >= 3) {
           // the boundary word patched once per half, read back from the staged
           // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
           // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
@@ -642,7 +642,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
             else
               r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
           }
-          const uint32_t z4t = s_z8half(lds, rc ^ wp.x, z8, 1);
+          // (variant 332, timing only: the ending frame's capture and Z_c skipped)
+          const uint32_t z4t = PATCH == 6 ? rc : s_z8half(lds, rc ^ wp.x, z8, 1);
           ecap = odd ? z4t ^ (wp.y & lm) : rc ^ (wp.x & lm);
         } else if constexpr (FOLD == 8) {
           // 8-byte units; the unit holding the boundary captures (r, w0, w1)
@@ -675,7 +676,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
         }
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
           uint32_t S = ecap;  // Z_c(e), c = 0..3
-          if constexpr (FOLD == 8) {
+          if constexpr (PATCH == 6) {
+          } else if constexpr (FOLD == 8) {
             // Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e) = ... T8_{8-c+i}[byte i]
             uint32_t y[3];
 #pragma unroll
@@ -716,6 +718,10 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     if constexpr (PF) asm volatile("" : "+v"(pre[0]), "+v"(pre[1]), "+v"(pre[2]), "+v"(pre[3]), "+v"(pre[4]), "+v"(pre[5]));
     asm volatile("" : "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]), "+v"(buf1[4]), "+v"(buf1[5]),
                  "+v"(buf1[6]), "+v"(buf1[7]));
+    if constexpr (PATCH == 7) {  // (variant 334, timing only: no carries)
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     // ---- carries: the true register at each stretch's start
     const uint32_t E1 = r;
     const bool hb = j > jstart;  // this stretch holds a boundary
@@ -771,9 +777,11 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
 #ifdef LNX_RESEARCH  // variants 300-303, 308, 309: both folds, 382- or 766-frame blocks
   // (10 waves per workgroup, variants 304-307, measured no faster in round 4
   // and no longer fit its registers once the whole line is read at once)
-  if (fold == 17 || fold == 18) {  // timing-only diagnostics of the product form (wrong results)
+  if (fold >= 17 && fold <= 20) {  // timing-only diagnostics of the product form (wrong results)
     if (fold == 17) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 4);
-    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 5);
+    else if (fold == 18) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 5);
+    else if (fold == 19) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 6);
+    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 7);
     return hipGetLastError();
   }
   if (fold == 16) {  // the product form with 6 waves (1.5 per SIMD): how much the second wave per SIMD buys

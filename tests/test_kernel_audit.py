@@ -68,8 +68,8 @@ def test_stage_kernel_passes_the_ring_audit(tmp_path):
                     "-o", str(tmp_path / "k.o"), path], cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
     syms = re.findall(r"^(_ZN3lnx18crc32_stage_kernel\w+):", open(tmp_path / asm).read(), flags=re.M)
-    assert len(syms) == 26  # CRC / verify x (the three folds, + 766-frame blocks, + the deferred correction,
-    #                          + the patched boundary word, + two chains per half, + 190- / 254-frame blocks, + offsets loaded a block ahead, + 510-frame blocks, + 6 waves, + 2 timing-only diagnostics)
+    assert len(syms) == 28  # CRC / verify x (the three folds, + 766-frame blocks, + the deferred correction,
+    #                          + the patched boundary word, + two chains per half, + 190- / 254-frame blocks, + offsets loaded a block ahead, + 510-frame blocks, + 6 waves, + 4 timing-only diagnostics)
     for sym in syms:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_ring.py"),
                             str(tmp_path / asm), sym], capture_output=True, text=True)
