@@ -375,9 +375,6 @@ def main():
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed launches for this long before the W warmup steps (GPU clock ramp)")
-    ap.add_argument("--event-every", type=int, default=10,
-                    help="bracket every N-th timed step with HIP events (kernel duration for the roofline); "
-                         "an event pair on every step adds a few microseconds of GPU idle per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-slice16m", action="store_true", help="skip the 16 M-frame equal-work sub-measurement")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -536,33 +533,34 @@ def main():
         dist.barrier()
     sync()
 
-    ev_every = max(1, args.event_every)
-    timed = list(range(0, args.steps, ev_every))
-    if cpu_ranks:  # host clock around the bracketed steps (no HIP events without a GPU)
+    # The roofline's launch time: one HIP-event window on the launch stream
+    # around all K timed steps (no event between steps, so the launches run
+    # back to back as in the untimed ones), divided by K.  It covers every
+    # launch of the entry (the plain CRC entry is the rows and the staged
+    # kernel, the one that owns no slice exiting at once: DESIGN.md §3.10).
+    if cpu_ranks:  # host clock around the window (no HIP events without a GPU)
         class _Ev:
             def record(self, _s):
                 self.t = time.perf_counter()
 
             def elapsed_time(self, e):
                 return (e.t - self.t) * 1e3
-        starts, ends = [_Ev() for _ in timed], [_Ev() for _ in timed]
+        ev0, ev1 = _Ev(), _Ev()
     else:
-        starts = [torch.cuda.Event(enable_timing=True) for _ in timed]
-        ends = [torch.cuda.Event(enable_timing=True) for _ in timed]
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        if k % ev_every == 0:
-            starts[k // ev_every].record(stream)
-            step()
-            ends[k // ev_every].record(stream)
-        else:
-            step()
+        step()
+    ev1.record(stream)
     sync()
     if dist:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    # the window sits inside the host clock's (both bracket the same launches)
+    assert cpu_ranks or kern_ms <= 1.01 * elapsed * 1e3 / args.steps, (kern_ms, elapsed * 1e3 / args.steps)
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=cdev)
     if dist:
@@ -608,6 +606,7 @@ def main():
             "bytes_per_gpu": nbytes,
             "parallelism": f"per-GPU frame partition x{world} (no collective)",
             "kernel": L.version(),
+            "build_id": L.build_id(),
         },
         "pct_hbm_peak": round(100.0 * (nbytes / (elapsed_max / args.steps) / 1e9) / HBM_PEAK_GBS, 2),
         "roofline": {
@@ -617,15 +616,17 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": ({"crc32": "lnx::crc32_stage_kernel<kCrc, 8, 8, 382, false, 1>",
-                        "fcs_verify": "lnx::crc32_stage_kernel<kVerify, 8, 8, 382, false, 1>"} if args.short_frames else {}).get(
-                args.op) or {"crc32": "lnx::crc32_rows_kernel<kCrc>", "fcs_verify": "lnx::crc32_rows_kernel<kVerify>",
+            "kernel": ({"crc32": "lnx::crc32_stage_kernel<kCrc>",
+                        "fcs_verify": "lnx::crc32_stage_kernel<kVerify>"} if args.short_frames else {}).get(
+                args.op) or {"crc32": "lnx::crc32_rows_kernel<kCrc> + lnx::crc32_stage_kernel<kCrc> (one entry; "
+                                      "each slice folded by the kernel slice_kind gives it, DESIGN.md §3.10)",
+                             "fcs_verify": "lnx::crc32_rows_kernel<kVerify> + lnx::crc32_stage_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
                        "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
             "kernel_ms": round(kern_ms, 4),
-            "kernel_ms_launches": len(timed),
+            "kernel_ms_window": f"HIP events around all {args.steps} timed steps on the launch stream, / {args.steps}",
             "algorithmic_bytes_per_launch": nbytes,
         },
     }
@@ -666,7 +667,8 @@ def main():
         comp["clock_ghz"] = round(clk / 1e9, 3)
         # counts from another build of the kernel say nothing about this one:
         # they are reported beside the HBM roofline, marked, and never replace it
-        comp["same_build"] = cn.get("lnx_version") == L.version()
+        # (the build is the code objects' hash, lneto_amd.build_id)
+        comp["same_build"] = cn.get("build_id") == L.build_id()
         out["roofline_compute"] = comp
         top = max(("valu", "lds"), key=lambda k: comp[k]["frac"])
         if comp["same_build"] and comp[top]["frac"] > out["roofline"]["frac"]:

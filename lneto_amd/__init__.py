@@ -21,7 +21,7 @@ import os
 __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
-    "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "LIB_PATH",
+    "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "build_id", "LIB_PATH",
     "CRC32_RESIDUE", "RxRing", "RxFilter", "RX_NO_FCS", "research_lib",
 ]
 
@@ -615,3 +615,32 @@ def device_count() -> int:
 
 def version() -> str:
     return lib.lnx_version().decode()
+
+
+def _elf_section(path: str, name: str) -> bytes:
+    """Bytes of section `name` of the ELF64 little-endian file at `path`."""
+    import struct
+    with open(path, "rb") as fh:
+        blob = fh.read()
+    if blob[:4] != b"\x7fELF" or blob[4] != 2 or blob[5] != 1:
+        raise ValueError(f"{path}: not an ELF64 little-endian file")
+    shoff, = struct.unpack_from("<Q", blob, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", blob, 0x3A)
+    def sh(i):
+        return struct.unpack_from("<IIQQQQIIQQ", blob, shoff + i * shentsize)
+    stroff = sh(shstrndx)[4]
+    for i in range(shnum):
+        nm, _, _, _, off, size = sh(i)[:6]
+        end = blob.index(b"\0", stroff + nm)
+        if blob[stroff + nm:end].decode() == name:
+            return blob[off:off + size]
+    raise KeyError(f"{path}: no section {name}")
+
+
+def build_id(path: str | None = None) -> str:
+    """sha256 (16 hex digits) of the gfx950 code objects (.hip_fatbin) of the
+    loaded library: the kernels' identity, unlike version(), a hand-written
+    string.  bench.py records it beside every line and compares it with the
+    one a committed PMC pass (profiles/counters_*.json) was taken on."""
+    import hashlib
+    return hashlib.sha256(_elf_section(path or LIB_PATH, ".hip_fatbin")).hexdigest()[:16]

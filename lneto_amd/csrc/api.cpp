@@ -13,14 +13,19 @@
 #include "gf2.hpp"
 #include "lds_layout.hpp"
 #include "rx_filter.hpp"
+#include "dispatch.hpp"
 
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                               bool verify, const void* image, int num_cus, hipStream_t stream);
+                               bool verify, const void* image, int num_cus, hipStream_t stream, uint32_t policy);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
-                              bool big_blocks = false);
+                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream);
 #ifdef LNX_RESEARCH
+namespace rs {
+hipError_t launch_crc32_stage_research(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
+                                       int fold, int waves, const void* image, int num_cus, hipStream_t stream,
+                                       bool big_blocks = false);
+}
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                                 const void* image, int num_cus, hipStream_t stream, uint64_t* timeline);
 uint64_t crc32_launch_waves(uint64_t n, int num_cus);
@@ -123,7 +128,7 @@ std::vector<uint32_t> build_lanes_image() {
 // tables A[e] = Z_2(e), B[e] = Z_1(e), then Z_{2^m} as eight nibble tables
 // for m = 0..30, entry (m, i, v) at dword 512 + 128 m + 16 i + v.
 std::vector<uint32_t> build_stage_image() {
-  std::vector<uint32_t> t(512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 4 * 1024);
+  std::vector<uint32_t> t(512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 4 * 1024 + 9 * 128);
   for (uint32_t e = 0; e < 256; ++e) t[e] = zshift_bytes(e, 2), t[256 + e] = zshift_bytes(e, 1);
   for (uint32_t m = 0; m < 31; ++m)
     for (uint32_t i = 0; i < 8; ++i)
@@ -140,6 +145,11 @@ std::vector<uint32_t> build_stage_image() {
     for (uint32_t k = 0; k < 4; ++k)
       for (uint32_t e = 0; e < 256; ++e)
         t[512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 1024 * z + 256 * k + e] = zshift_bytes(e << (8 * k), 8 * (z + 1));
+  for (uint32_t m = 31; m < 40; ++m)  // Z_{2^m} nibble tables for m = 31..39 (giant frames' Z_d, stage_kernel.hip)
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v)
+        t[512 + 31 * 128 + 1024 + 2048 + 3 * 1024 + 4 * 1024 + 128 * (m - 31) + 16 * i + v] =
+            zshift_bytes_fast(v << (4 * i), 1ull << m);
   return t;
 }
 
@@ -206,6 +216,15 @@ struct DeviceCtx {
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
   uint32_t* d_stage = nullptr;   // crc32_stage_kernel image
+  // Per stream: the staged kernel's giant-slice slots (stage_kernel.hip
+  // giant_pieces; zero between launches).  Launches on one stream run in
+  // order, so each stream owns one set; streams never share one.
+  struct GiantScratch {
+    hipStream_t stream;
+    uint32_t* p;
+  };
+  std::mutex giant_mu;
+  std::vector<GiantScratch> giant;
 #ifdef LNX_RESEARCH
   // Per-stream scratch of the two-launch TX append (the CRCs between its
   // launches): calls on one stream run in order, so each stream reuses its
@@ -306,28 +325,62 @@ int get_ctx(DeviceCtx** out) {
   return LNX_OK;
 }
 
-// The staged lane-stream form the product uses for LNX_BATCH_SHORT_FRAMES
-// (stage_kernel.hip): the slicing-by-8 fold in 8 rotated bank
-// columns, 8 waves per workgroup.
-constexpr int kStageFold = 8, kStageWaves = 8;
+// Slots of the giant slices: acc[kGiantSlots] then cnt[kGiantSlots]
+// (stage_kernel.hip: at most 2^20 pieces plus one per slice)
+constexpr size_t kGiantSlots = (1u << 20) + 4096u;
 
+// The calling device's giant-slice scratch for `stream`, zeroed once when made.
+int giant_scratch(DeviceCtx* c, hipStream_t stream, uint32_t** out) {
+  std::lock_guard<std::mutex> lk(c->giant_mu);
+  for (const auto& g : c->giant)
+    if (g.stream == stream) {
+      *out = g.p;
+      return LNX_OK;
+    }
+  uint32_t* p = nullptr;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), 2 * kGiantSlots * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(giant-slice scratch)");
+  if ((e = hipMemset(p, 0, 2 * kGiantSlots * sizeof(uint32_t))) != hipSuccess) {
+    (void)hipFree(p);
+    return hip_fail(e, "hipMemset(giant-slice scratch)");
+  }
+  c->giant.push_back({stream, p});
+  *out = p;
+  return LNX_OK;
+}
+
+}  // namespace
+
+// CRC-32 / FCS verify of an offsets batch: the rows kernel,
+// then the staged kernel, over the same slices; each workgroup folds its slice
+// only if dispatch.hpp's slice_kind() gives it to its kernel, and the staged
+// launch folds the giant slices.  policy kPolicyShort (LNX_BATCH_SHORT_FRAMES)
+// gives every slice that fits to the staged kernel, so the rows launch is
+// skipped.  Also the receive ring's entry (rx_ring.hip).
+int crc_offsets(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify, uint32_t policy,
+                hipStream_t stream) {
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  uint32_t* scratch = nullptr;
+  if ((st = giant_scratch(c, stream, &scratch)) != LNX_OK) return st;
+  hipError_t e = hipSuccess;
+  if (policy == kPolicyAuto) e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus, stream, policy);
+  if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel launch");
+  e = launch_crc32_stage(d_bytes, d_off, n, d_out, verify, policy, c->d_stage, scratch, c->num_cus, stream);
+  if (e != hipSuccess) return hip_fail(e, "crc32_stage_kernel launch");
+  return LNX_OK;
+}
+
+namespace {
 int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify,
                uint32_t flags, void* stream) {
   if (flags & ~LNX_BATCH_SHORT_FRAMES) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   if (!d_bytes || !d_off || !d_out) return LNX_EINVAL;
-  DeviceCtx* c = nullptr;
-  int st = get_ctx(&c);
-  if (st != LNX_OK) return st;
-  hipError_t e = (flags & LNX_BATCH_SHORT_FRAMES)
-                     ? launch_crc32_stage(d_bytes, d_off, n, d_out, verify, kStageFold, kStageWaves, c->d_stage,
-                                          c->num_cus, static_cast<hipStream_t>(stream))
-                     : launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus,
-                                           static_cast<hipStream_t>(stream));
-  if (e != hipSuccess) return hip_fail(e, "crc32 batch launch");
-  return LNX_OK;
+  return crc_offsets(d_bytes, d_off, n, d_out, verify, (flags & LNX_BATCH_SHORT_FRAMES) ? kPolicyShort : kPolicyAuto,
+                     static_cast<hipStream_t>(stream));
 }
-
 }  // namespace
 
 // For the other translation units (rx_ring.hip): the current device's LDS
@@ -526,10 +579,8 @@ int lnx_crc32_batch_host(const uint8_t* h_bytes, uint64_t nbytes, const uint64_t
         (e = hipMemcpyAsync(d_off, h_off, (n + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess)
       rc = hip_fail(e, "hipMemcpyAsync H2D");
   }
-  // the host knows this batch's mix: short-frame batches take the staged kernel
-  const uint32_t flags = (h_off[n] > h_off[0] ? h_off[n] - h_off[0] : 0) < (uint64_t)n * LNX_SHORT_FRAME_MEAN
-                             ? LNX_BATCH_SHORT_FRAMES : 0u;
-  if (rc == LNX_OK) rc = lnx_crc32_batch_ex(d_bytes, d_off, n, d_crc, flags, s);
+  // (the plain entry: each slice's kernel is picked on the device)
+  if (rc == LNX_OK) rc = lnx_crc32_batch(d_bytes, d_off, n, d_crc, s);
   if (rc == LNX_OK && (e = hipMemcpyAsync(h_crc, d_crc, n * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
     rc = hip_fail(e, "hipMemcpyAsync D2H");
   if (d_bytes) (void)hipFreeAsync(d_bytes, s);
@@ -586,10 +637,14 @@ int lnx__crc32_variant(int var, const uint8_t* d_bytes, const uint64_t* d_off, u
   // 324 / 325: 314 / 315 with 510-frame blocks; 326 / 327: 314 / 315 with 6 waves;
   // 328 / 330: timing only (wrong results): 314 without the transpose writes,
   // 314 with a two-op stand-in for the lookups; 332: 314 without the ending
-  // frames' capture and Z_c; 334: 314 without the carries
-  hipError_t e = (var >= 300 && var <= 327) || var == 328 || var == 330 || var == 332 || var == 334
-                     ? launch_crc32_stage(d_bytes, d_off, n, d_crc, var & 1,
-                                          var == 334 ? 20 : var == 332 ? 19 : var == 330 ? 18 : var == 328 ? 17 : var >= 326 ? 16 : var >= 324 ? 15 : var >= 322 ? 14 : var >= 320 ? 13 : var >= 318 ? 12 : var >= 316 ? 11 : var >= 314 ? 10 : var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
+  // frames' capture and Z_c; 334: 314 without the carries; 340: the ring's
+  // loads alone; 342: loads + the LDS transpose (round 5)
+  // (all in stage_research.hip, the round-4 kernel; the product staged kernel
+  // with its round-5 dispatch is lnx_crc32_batch_ex(LNX_BATCH_SHORT_FRAMES))
+  hipError_t e = (var >= 300 && var <= 327) || var == 328 || var == 330 || var == 332 || var == 334 || var == 340 ||
+                         var == 342
+                     ? rs::launch_crc32_stage_research(d_bytes, d_off, n, d_crc, var & 1,
+                                          var == 342 ? 22 : var == 340 ? 21 : var == 334 ? 20 : var == 332 ? 19 : var == 330 ? 18 : var == 328 ? 17 : var >= 326 ? 16 : var >= 324 ? 15 : var >= 322 ? 14 : var >= 320 ? 13 : var >= 318 ? 12 : var >= 316 ? 11 : var >= 314 ? 10 : var >= 312 ? 9 : var >= 310 ? 8 : (var & 2) || var >= 308 ? 4 : 2,
                                           var >= 304 && var < 308 ? 10 : 8, c->d_stage, c->num_cus,
                                           static_cast<hipStream_t>(stream), var == 308 || var == 309)
                      : launch_crc32_variant(var, d_bytes, d_off, n, d_crc, c->d_image, c->num_cus,

@@ -47,6 +47,7 @@
 #include <type_traits>
 #include <utility>
 #include "lds_layout.hpp"
+#include "dispatch.hpp"
 
 // Cache-policy suffix of the streaming frame loads (e.g. " nt" for profiling
 // builds: make CXXFLAGS+='-DLNX_LD_POL=\"\ nt\"').  Default policy by default.
@@ -1529,7 +1530,7 @@ __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the FCS through it */ const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
                   uint64_t* __restrict__ timeline,
-                  const uint32_t* seg_len, uint32_t cap) {
+                  const uint32_t* seg_len, uint32_t cap, uint32_t policy) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path
@@ -1537,6 +1538,9 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
   const uint64_t per_block = frames_per_wave * kWavesPerBlock;
   const uint64_t fb0 = (uint64_t)blockIdx.x * per_block < nframes ? (uint64_t)blockIdx.x * per_block : nframes;
   const uint64_t fb1 = fb0 + per_block < nframes ? fb0 + per_block : nframes;
+  // the plain entries launch this kernel and the staged one over the same
+  // slices (dispatch.hpp): a slice that is not the rows kernel's exits here
+  if (!SEG && policy != kPolicyRows && slice_kind(bytes, off, fb0, fb1, policy) != kSliceRows) return;
   // byte bounds of frames [f0, f1): offsets mode off[f0], off[f1]; segment
   // mode (frames in address order, not overlapping) start[f0], end of f1 - 1
   auto lo_of = [&](uint64_t f0, uint64_t f1) -> uint64_t { return SEG ? (f1 > f0 ? off[f0] : 0) : off[f0]; };
@@ -1708,19 +1712,20 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
 
 hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                        const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr,
-                       const uint32_t* seg_len = nullptr, uint32_t cap = 0) {
+                       const uint32_t* seg_len = nullptr, uint32_t cap = 0, uint32_t policy = kPolicyRows) {
   const bool verify = mode == CrcMode::kVerify;
   if (n == 0) return hipSuccess;
-  const uint64_t per_block = (uint64_t)kWavesPerBlock * 4;  // one 16-lane row set per wave at least
-  uint64_t grid = (n + per_block - 1) / per_block;
-  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
-  const uint64_t waves = grid * kWavesPerBlock;
-  const uint64_t fpw = (n + waves - 1) / waves;
+  // the slices of dispatch.hpp (the staged launch uses the same): at least
+  // one 16-lane row set per wave
+  const SlicePlan pl = slice_plan(n, num_cus);
+  static_assert(kWavesPerBlock == 16, "slice_plan's slices are whole 16-wave sets");
+  const uint64_t grid = pl.grid;
+  const uint64_t fpw = pl.per / kWavesPerBlock;
   const uint4* img = static_cast<const uint4*>(images);
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
-                     timeline, seg_len, cap)
+                     timeline, seg_len, cap, policy)
   if (seg_len) {  // segment mode (lnx_crc32_segments, the TX FCS append, the receive ring)
     // (every lean-row step non-temporal, EP = 0, was measured no faster for
     // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
@@ -1855,8 +1860,9 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
 
 // Host-side launch helpers (called from api.cpp).
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                               const void* images, int num_cus, hipStream_t stream) {
-  return launch_rows(0, verify ? CrcMode::kVerify : CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream);
+                               const void* images, int num_cus, hipStream_t stream, uint32_t policy) {
+  return launch_rows(0, verify ? CrcMode::kVerify : CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream,
+                     nullptr, nullptr, 0, policy);
 }
 #ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,

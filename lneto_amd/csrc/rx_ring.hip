@@ -47,12 +47,9 @@
 namespace lnx {
 
 int device_resources(const void** image, int* num_cus, const void** stage_image);
-hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
-                              bool big_blocks = false);
+int crc_offsets(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify, uint32_t policy,
+                hipStream_t stream);
 int hip_error(hipError_t e, const char* what);
-hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                               const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                       uint8_t* ok, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
@@ -186,14 +183,14 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
     if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
         (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess)
       return hip_error(e, "rx ring H2D (packed)");
-    // a packed batch of short frames (the host knows its mix) takes the staged
-    // lane streams, a batch of long ones the row kernel
-    const bool short_mix = total < (uint64_t)nb * LNX_SHORT_FRAME_MEAN;
-    e = !fcs ? hipMemsetAsync(s.d_ok, 1, nb, s.s)
-        : short_mix ? launch_crc32_stage(s.d_bytes, s.d_start, nb, s.d_ok, true, 8, 8, r->stage_image, r->num_cus,
-                                         s.s)
-                    : launch_crc32_frames(s.d_bytes, s.d_start, nb, s.d_ok, true, r->image, r->num_cus, s.s);
-    if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");
+    // the packed batch's FCS verify: lnx_fcs_verify_batch's dispatch (the
+    // rows or the staged kernel per slice)
+    if (!fcs) {
+      if ((e = hipMemsetAsync(s.d_ok, 1, nb, s.s)) != hipSuccess) return hip_error(e, "rx ring FCS verify memset");
+    } else {
+      const int rc = crc_offsets(s.d_bytes, s.d_start, nb, s.d_ok, true, 0u /* kPolicyAuto */, s.s);
+      if (rc != LNX_OK) return rc;
+    }
     if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, nullptr, trim,
                                    &r->filt)) != hipSuccess)
       return hip_error(e, "rx ring ingress verify launch");

@@ -1,21 +1,20 @@
 // stage_kernel.hip — batched CRC-32 / FCS verify by staged lane streams, gfx950
-// (round 4).  Reference semantics: ethernet.CRC32 (lneto
-// ethernet/crc.go:19-21) = Go crc32.Checksum(data, IEEETable); the verify mode
-// is the residue form of the FCS check.  The schedule is restated on the host
-// in tests/stage_algebra.py and checked there against zlib.
+// (round 4, the product form since round 5).
+// Reference semantics: ethernet.CRC32 (lneto ethernet/crc.go:19-21) =
+// Go crc32.Checksum(data, IEEETable); the verify mode is the residue form of
+// the FCS check.  The schedule is restated on the host in
+// tests/stage_algebra.py and checked there against zlib.
 //
-// Why: on short frames (the Zipf mix, mean 246 B) every per-frame window
-// layout is bound by the L2 request rate (a line two frames share is asked for
-// twice, a short frame's partial lines cost a request each).
-// Here each line is requested once, whole, and a lane still folds a
-// CONTIGUOUS byte stream, so a frame boundary costs no cross-lane work:
+// Why: on mixed-length frames (the Zipf mix, mean 246 B) every per-frame
+// window layout is bound by the L2 request rate (a line two frames share is
+// asked for twice, a short frame's partial lines cost a request each;
+// DESIGN.md §4).  Here each line is requested once, whole, and a lane still
+// folds a CONTIGUOUS byte stream, so a frame boundary costs no cross-lane work:
 //
 //  * a wave takes a block of kStageBF consecutive frames, bytes [A, E), and
 //    cuts 64 stretches of Q bytes (Q a multiple of 128) from A rounded down to
-//    128; lane k folds stretch k one dword at a time, r <- Z4(r ^ w), through
-//    lane-private slicing-by-2 tables (Z4 = Z2 o Z2, Z2(v) = (v >> 16) ^
-//    A[v & 0xFF] ^ B[(v >> 8) & 0xFF]; 64 KiB instead of the 128 KiB of
-//    slicing-by-4, which leaves LDS for the staging);
+//    128; lane k folds stretch k eight bytes at a time through lane-private
+//    slicing-by-8 tables, r <- Z8(r ^ w0) ^ Z4(w1);
 //  * per round each lane needs its stretch's next 128-byte line: 8
 //    buffer_load_dwordx4, instruction m / lane t reading piece
 //    ((t & 7) - s) & 7 of stretch s = 8 (t >> 3) + m, so every instruction
@@ -24,17 +23,26 @@
 //    1024 (s & 7) + 128 (s >> 3) + 16 ((i + s) & 7), conflict-free;
 //  * a boundary x (an offset of the block) in the dword at 4d, byte c:
 //    e = r ^ (w & lomask(c)), the ending frame's state is Z_c(e) (its CRC the
-//    complement); r <- Z4((w & ~lomask(c)) ^ K_c), K_c = Z_{-c}(~0), is the
-//    new frame's state after the dword from the CRC init.  One boundary per
-//    64-byte half is handled by selects inside the fold; a half where some
-//    lane has two (frames under 64 bytes, empty frames) runs byte by byte;
+//    complement); the new frame's chain starts from the patched word
+//    (w & ~lomask(c)) ^ K_c, K_c = Z_{-c}(~0).  One boundary per 64-byte half
+//    is handled inside the fold; a half where some lane has two (frames under
+//    64 bytes, empty frames) runs byte by byte;
 //  * a stretch starts inside a frame: its first boundary's state is local.
 //    After the block, P_k (the true register at stretch k's start) is the
 //    previous lane's end register (or, past a frame longer than a stretch,
 //    Z_Q(P_{k-1}) ^ E_{k-1}), and the first frame's state gains Z_d(P_k),
 //    d = x - S_k, by binary powers Z_{2^m} from shared nibble tables.
+//
+// Round 5: the kernel is the second launch behind the plain
+// entries.  A workgroup folds its slice only when dispatch.hpp's slice_kind()
+// gives it to this kernel; every workgroup then folds its share of the giant
+// slices (bytes past 31-bit buffer offsets) in byte pieces, one piece per
+// lane, the parts of a frame that crosses pieces joined by Z_d shifts and
+// device-scope XORs into a per-stream scratch (giant_pieces below).  A block
+// whose offsets are out of order is folded one lane per frame (ooo_block).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include "dispatch.hpp"
 
 namespace lnx {
 
@@ -43,43 +51,29 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 enum class StageMode : int { kCrc = 0, kVerify = 1 };
 
 constexpr uint32_t kStageBF = 382;  // frames per block: the boundary list (bf + 1 + 2 sentinels) fits 384 dwords
-constexpr uint32_t kStageBFBig = 766;  // variants 308 / 309: 768-dword lists, half the per-block overhead
-constexpr uint32_t kStageBFSmall = 190, kStageBFMid = 254;  // variants 318-321: shorter blocks, a shorter tail
-constexpr uint32_t kStageBF510 = 510;  // variants 324 / 325: the longest lists that leave the nibble tables in LDS
-// LDS layout (bytes) for W waves per workgroup.  W = 8: the Z_{2^m} nibble
-// tables live in LDS too; W = 10 (variants 304-307): they are read from the
-// image in HBM (only the carries use them, once per stretch), which frees the
-// room for two more waves' transposes and lists.
-constexpr uint32_t kSTab = 0;  // A (Z_2) / B (Z_1): e << 8 | m << 7 | c << 2
-template <int W, uint32_t BF = kStageBF, uint32_t ZXB = 0>
-struct StageLds {
-  static_assert((BF + 2) % 64 == 0, "whole-wave list loads");
-  static constexpr uint32_t kList = (BF + 2) * 4;      // boundary list bytes per wave (bf + 1 entries + sentinel)
-  static constexpr uint32_t kTr = 65536;               // transposes: 8 KiB per wave
-  static constexpr uint32_t kBnd = kTr + W * 8192;     // boundary lists
-  // ZXB bytes of shared single-column byte tables after the lists: Z_16, Z_32,
-  // Z_64 (DEFER, variants 312 / 313, 12 KiB) or Z_8, Z_16, Z_24, Z_32 (two
-  // chains per half, variants 316 / 317, 16 KiB); the nibble tables then
-  // stay in HBM
-  static constexpr uint32_t kZx = kBnd + W * kList;
-  static constexpr uint32_t kZxBytes = ZXB;
-  static constexpr bool kNibInLds = ZXB == 0 && kBnd + W * kList + 31 * 512 + 16 <= 163840;
-  static constexpr uint32_t kNib = kZx + kZxBytes;     // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
-  static constexpr uint32_t kCtr = kNib + (kNibInLds ? 31 * 512 : 0);  // the workgroup's block counter
-  static constexpr uint32_t kBytes = kCtr + 16;
-  static_assert(kBytes <= 163840, "stage LDS");
-};
-// compact image in HBM (api.cpp build_stage_image): A[256], B[256], then the
-// nibble tables verbatim (512 + 31 * 128 dwords), then (FOLD 4) the four Z_4
-// byte tables, table k entry e at kStageZ4Img + 256 k + e
-constexpr uint32_t kStageZ4Img = 512 + 31 * 128;
-// then (FOLD 8) the eight slicing-by-8 byte tables T8_k[e] = Z_{8-k}(e), table
-// k entry e at kStageZ8Img + 256 k + e
-constexpr uint32_t kStageZ8Img = kStageZ4Img + 1024;
-// then (DEFER) Z_16, Z_32, Z_64 as four byte tables each: (t, k, e) at kStageZxImg + 1024 t + 256 k + e
-constexpr uint32_t kStageZxImg = kStageZ8Img + 2048;
-// then (two chains per half) Z_8, Z_16, Z_24, Z_32: (t, k, e) at kStageZyImg + 1024 t + 256 k + e = Z_{8(t+1)}(e << 8k)
-constexpr uint32_t kStageZyImg = kStageZxImg + 3072;
+constexpr uint32_t kStageW = 8;     // waves per workgroup (two per SIMD: 182-193 VGPRs each)
+// LDS layout (bytes)
+constexpr uint32_t kSTab = 0;                          // T8_k tables: e << 8 | k << 5 | c << 2 (64 KiB)
+constexpr uint32_t kSList = (kStageBF + 2) * 4;         // boundary list bytes per wave
+constexpr uint32_t kSTr = 65536;                        // transposes: 8 KiB per wave
+constexpr uint32_t kSBnd = kSTr + kStageW * 8192;       // boundary lists
+constexpr uint32_t kSNib = kSBnd + kStageW * kSList;    // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
+constexpr uint32_t kSCtr = kSNib + 31 * 512;            // the workgroup's block counter
+constexpr uint32_t kSBytes = kSCtr + 16;
+static_assert(kSBytes <= 163840, "stage LDS");
+static_assert((kStageBF + 2) % 64 == 0, "whole-wave list loads");
+// compact image in HBM (api.cpp build_stage_image): A[256], B[256], the
+// nibble tables of Z_{2^m} for m = 0..30 (512 + 128 m + 16 i + v), the Z_4
+// byte tables, the slicing-by-8 byte tables T8_k[e] = Z_{8-k}(e) at
+// kStageZ8Img + 256 k + e, the research tables, then the nibble tables of
+// Z_{2^m} for m = 31..39 at kStageNibHiImg + 128 (m - 31) + 16 i + v
+constexpr uint32_t kStageZ8Img = 512 + 31 * 128 + 1024;
+constexpr uint32_t kStageNibHiImg = kStageZ8Img + 2048 + 3072 + 4096;
+// giant slices: pieces of at least this many bytes, at most kGiantPieces of them
+constexpr uint64_t kGiantPieceMin = 16384;
+constexpr uint32_t kGiantPieces = 1u << 20;
+// a frame of an out-of-order block longer than this is not folded (result 0)
+constexpr uint64_t kOooMaxFrame = 1ull << 20;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -87,32 +81,18 @@ constexpr uint32_t kSNone = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t s_lds(const char* lds, uint32_t a) {
   return *reinterpret_cast<const uint32_t*>(lds + a);
 }
-// Z_2(v) through the lane-private tables (b0 = this lane's column << 2)
-__device__ __forceinline__ uint32_t s_z2(const char* lds, uint32_t v, uint32_t b0) {
-  const uint32_t a = __builtin_amdgcn_perm(v, b0, 0x0c020400u), b = __builtin_amdgcn_perm(v, b0, 0x0c020500u);
-  return __builtin_amdgcn_bitop3_b32(v >> 16, s_lds(lds, kSTab + a), s_lds(lds, kSTab + b + 128u), 0x96);
-}
-// FOLD 2: Z_1 is table B.  FOLD 4 (variants 302 / 303): the four Z_4 byte
-// tables in 16 bank columns, entry e of table k, column c at e << 8 | k << 6 |
-// c << 2 (64 KiB like FOLD 2's), one LDS round trip per dword instead of two;
-// Z_1 is its table 3 (Z_4(e << 24) = Z_1(e)).  Lanes c and c + 16 share column
-// c, and table k sits in bank half k & 1, so the k-th lookup of lane half h =
-// (lane >> 4) & 1 reads table (k + h) & 3: in every instruction the two halves
-// of a 32-lane pass read opposite bank halves (conflict-free; the XOR of the
-// four lookups does not depend on their order).
-template <int FOLD>
+// Z_1(v): the T8_7 table
 __device__ __forceinline__ uint32_t s_z1(const char* lds, uint32_t v, uint32_t b0) {
-  return (v >> 8) ^
-         s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + (FOLD == 8 ? 224u : FOLD == 4 ? 192u : 128u));
+  return (v >> 8) ^ s_lds(lds, kSTab + __builtin_amdgcn_perm(v, b0, 0x0c020400u) + 224u);
 }
-// FOLD 8 (variants 310 / 311): slicing-by-8 over 8-byte units, the eight byte
-// tables T8_k[e] = Z_{8-k}(e) in 8 bank columns, entry e of table k, column c
-// at e << 8 | k << 5 | c << 2 (64 KiB).  A unit (w0, w1) entered with r leaves
-// Z_8(r ^ w0) ^ Z_4(w1) = XOR_k T8_k[byte k of r ^ w0] ^ XOR_k T8_{4+k}[byte k
-// of w1]: the w1 half is off the chain, so a lane's chain takes one LDS round
-// trip per 8 bytes.  Table k sits in bank octet k & 3; the four 8-lane groups
-// g = (lane >> 3) & 3 of a pass read tables (i + g) & 3 (and 4 + that) in
-// lookup i, so each lookup instruction is conflict-free.
+// Slicing-by-8 over 8-byte units, the eight byte tables T8_k[e] = Z_{8-k}(e)
+// in 8 bank columns, entry e of table k, column c at e << 8 | k << 5 | c << 2
+// (64 KiB).  A unit (w0, w1) entered with r leaves Z_8(r ^ w0) ^ Z_4(w1) =
+// XOR_k T8_k[byte k of r ^ w0] ^ XOR_k T8_{4+k}[byte k of w1]: the w1 half is
+// off the chain, so a lane's chain takes one LDS round trip per 8 bytes.
+// Table k sits in bank octet k & 3; the four 8-lane groups g = (lane >> 3) & 3
+// of a pass read tables (i + g) & 3 (and 4 + that) in lookup i, so each
+// lookup instruction is conflict-free.
 struct Z8Lane {
   uint32_t base[8], sel[4];  // base[i] (table (i + g) & 3), base[4 + i] (table 4 + ((i + g) & 3))
   __device__ explicit Z8Lane(uint32_t lane) {
@@ -144,55 +124,36 @@ __device__ __forceinline__ uint32_t s_z8unit(const char* lds, uint32_t v0, uint3
   const uint32_t t = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(y[4], y[5], y[6], 0x96), y[7], y[0], 0x96);
   return __builtin_amdgcn_bitop3_b32(t, y[1], y[2], 0x96) ^ y[3];
 }
-// the FOLD 4 lookups' per-lane v_perm bases / selectors: lookup i reads table
-// k = (i + h) & 3 at byte (v.byte_k << 8) | (k << 6) | (c << 2)
-struct Z4Lane {
-  uint32_t base[4], sel[4];
-  __device__ explicit Z4Lane(uint32_t lane) {
-    const uint32_t h = (lane >> 4) & 1u, c = lane & 15u;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) {
-      const uint32_t k = (i + h) & 3u;
-      base[i] = (k << 6) | (c << 2);
-      sel[i] = 0x0c020400u + (k << 8);
-    }
-  }
-};
-// Z_4(v)
-template <int FOLD>
-__device__ __forceinline__ uint32_t s_z4(const char* lds, uint32_t v, uint32_t b0, const Z4Lane& zl) {
-  if constexpr (FOLD == 4) {
-    uint32_t y[4];
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(v, zl.base[i], zl.sel[i]));
-    return __builtin_amdgcn_bitop3_b32(y[0], y[1], y[2], 0x96) ^ y[3];
-  } else {
-    return s_z2(lds, s_z2(lds, v, b0), b0);
-  }
-}
 
-// Z_{2^m}(v) through the shared nibble tables (every lane reads table m: a
-// nibble value picks one of 16 banks, equal values broadcast), from LDS or,
-// for W > 8, from the image in HBM (dword (m, i, v) at 512 + 128 m + 16 i + v)
-template <class LY>
-__device__ __forceinline__ uint32_t s_zpow2(const char* lds, const uint32_t* image, uint32_t m, uint32_t v) {
+// Z_{2^m}(v), m <= 30, through the shared nibble tables in LDS (every lane
+// reads table m: a nibble value picks one of 16 banks, equal values broadcast)
+__device__ __forceinline__ uint32_t s_zpow2(const char* lds, uint32_t m, uint32_t v) {
   uint32_t a = 0;
-  if constexpr (LY::kNibInLds) {
-    const uint32_t t = LY::kNib + 512u * m;
+  const uint32_t t = kSNib + 512u * m;
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
-  } else {
-    const uint32_t* t = image + 512u + 128u * m;
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) a ^= t[16u * i + __builtin_amdgcn_ubfe(v, 4 * i, 4)];
-  }
+  for (uint32_t i = 0; i < 8; ++i) a ^= s_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
   return a;
 }
 // Z_d(v), d < 2^31, by binary powers; lanes whose d is done keep their value
-template <class LY>
-__device__ __forceinline__ uint32_t s_zd(const char* lds, const uint32_t* image, uint32_t d, uint32_t v) {
+__device__ __forceinline__ uint32_t s_zd(const char* lds, uint32_t d, uint32_t v) {
   for (uint32_t m = 0; __builtin_amdgcn_ballot_w64((d >> m) != 0u) != 0; ++m) {
-    const uint32_t z = s_zpow2<LY>(lds, image, m, v);
+    const uint32_t z = s_zpow2(lds, m, v);
+    v = ((d >> m) & 1u) ? z : v;
+  }
+  return v;
+}
+// Z_d(v), d < 2^40 (giant frames): m > 30 from the image in HBM
+__device__ __forceinline__ uint32_t s_zd64(const char* lds, const uint32_t* image, uint64_t d, uint32_t v) {
+  for (uint32_t m = 0; __builtin_amdgcn_ballot_w64((d >> m) != 0u) != 0; ++m) {
+    uint32_t z;
+    if (m <= 30) {
+      z = s_zpow2(lds, m, v);
+    } else {
+      const uint32_t* t = image + kStageNibHiImg + 128u * (m - 31u);
+      z = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i) z ^= t[16u * i + __builtin_amdgcn_ubfe(v, 4 * i, 4)];
+    }
     v = ((d >> m) & 1u) ? z : v;
   }
   return v;
@@ -209,65 +170,277 @@ constexpr uint32_t s_unz(uint32_t v, int nbytes) {
 }
 constexpr uint32_t kK1 = s_unz(0xFFFFFFFFu, 1), kK2 = s_unz(0xFFFFFFFFu, 2), kK3 = s_unz(0xFFFFFFFFu, 3);
 
-template <StageMode MODE, int FOLD, int W, uint32_t BF = kStageBF, bool DEFER = false, int PATCH = 0>
-__global__ void __launch_bounds__(W * 64, 1)
+template <StageMode MODE>
+__device__ __forceinline__ uint32_t stage_value(uint32_t reg, uint64_t len) {
+  const uint32_t crc = ~reg;
+  return MODE == StageMode::kCrc ? crc : (uint32_t)(len >= 4 && crc == 0x2144DF1Cu);
+}
+
+template <StageMode MODE>
+__device__ __forceinline__ void stage_store(void* out, uint64_t f, uint32_t v) {
+  if constexpr (MODE == StageMode::kCrc)
+    reinterpret_cast<uint32_t*>(out)[f] = v;
+  else
+    reinterpret_cast<uint8_t*>(out)[f] = (uint8_t)v;
+}
+
+// ---------------------------------------------------------------- out of order
+// A block whose offsets are not non-decreasing (outside the entry's contract;
+// a frame whose end is below its start is empty, as in the rows kernel): one
+// lane per frame, byte by byte, the whole wave looping to the longest frame
+// (a lane past its frame re-reads its first byte and keeps its register, so
+// no load issues under narrowed exec — the audit's loop rule).
+// Frames longer than kOooMaxFrame are not folded (result 0 / not ok), which
+// bounds the loop.
+template <StageMode MODE>
+__device__ __forceinline__ void ooo_block(const char* lds, const uint8_t* bytes, const uint64_t* off, uint64_t f0, uint32_t bf,
+                          void* out, uint32_t lane, uint32_t b0) {
+  for (uint32_t j0 = 0; j0 < bf; j0 += 64u) {
+    const uint32_t j = j0 + lane;
+    const uint64_t s = j < bf ? off[f0 + j] : 0, e0 = j < bf ? off[f0 + j + 1] : 0;
+    const uint64_t len0 = e0 > s ? e0 - s : 0;
+    const uint64_t len = len0 > kOooMaxFrame ? 0 : len0;
+    uint32_t r = 0xFFFFFFFFu;
+    for (uint64_t q = 0;; ++q) {
+      const bool act = q < len;
+      if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+      uint32_t b = 0;
+      if (act) b = bytes[s + q];  // (single bytes: no multi-dword load under a narrowed exec)
+      const uint32_t nr = s_z1(lds, r ^ b, b0);
+      r = act ? nr : r;
+    }
+    if (j < bf) stage_store<MODE>(out, f0 + j, len0 > kOooMaxFrame ? 0u : stage_value<MODE>(r, len));
+  }
+}
+
+// ---------------------------------------------------------------- giant slices
+// Every workgroup of the launch folds its share of the giant slices (their
+// bytes do not fit 31-bit buffer offsets).  The bytes of all
+// giant slices are cut into NP pieces of P bytes (P = max(16 KiB, total / 2^20
+// rounded up to 16 KiB), so NP <= 2^20 + #slices); global lane t folds pieces
+// t, t + T, ... (T lanes in the launch).  A lane folds its piece [a, b) as one
+// byte stream in 128-byte blocks (8 dwordx4 loads, wave-uniform trip count),
+// eight bytes per step through the lane-private tables; a block holding a
+// frame boundary or a piece edge in some lane is folded byte by byte from LDS
+// for the whole wave.  A frame inside one piece is finished there; a frame
+// that crosses pieces gets, from each piece it touches, its register there
+// advanced to the frame end, Z_{e - v}(r) (v = the end of its part in the
+// piece), XORed into the scratch slot of the first piece boundary it crosses
+// (device-scope atomics: the XOR, then a release/acquire count); the lane
+// whose count completes the frame takes the XOR (leaving the slot zero for
+// the next launch) and stores the result.  Offsets must be non-decreasing in
+// giant slices.
+template <StageMode MODE>
+__device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* image, const uint8_t* bytes, const uint64_t* off,
+                             uint64_t nframes, uint64_t per, void* out, uint32_t* scratch, char* tr, uint32_t* pre,
+                             uint32_t lane, uint32_t b0, const Z8Lane& z8) {
+  const uint32_t G = gridDim.x;
+  // ---- the giant slices, their total bytes and the piece prefix pre[0..G] (LDS)
+  uint64_t tg = 0;
+  for (uint32_t w0 = 0; w0 < G; w0 += 64u) {
+    const uint32_t w = w0 + lane;
+    const uint64_t f0 = (uint64_t)w * per < nframes ? (uint64_t)w * per : nframes;
+    const uint64_t f1 = f0 + per < nframes ? f0 + per : nframes;
+    const uint64_t s = off[f0], e = off[f1];
+    const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
+    const bool gi = w < G && slice_is_giant(span, adj, f1 - f0);
+    tg += gi ? span : 0;
+  }
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) tg += (uint64_t)__shfl_xor((long long)tg, sft);
+  uint64_t P = (tg + kGiantPieces - 1) / kGiantPieces;
+  P = (P + kGiantPieceMin - 1) / kGiantPieceMin * kGiantPieceMin;
+  P = P < kGiantPieceMin ? kGiantPieceMin : P;
+  P = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)P)) |
+      ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(P >> 32)) << 32);
+  uint32_t carry = 0;
+  for (uint32_t w0 = 0; w0 < G; w0 += 64u) {
+    const uint32_t w = w0 + lane;
+    const uint64_t f0 = (uint64_t)w * per < nframes ? (uint64_t)w * per : nframes;
+    const uint64_t f1 = f0 + per < nframes ? f0 + per : nframes;
+    const uint64_t s = off[f0], e = off[f1];
+    const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
+    const bool gi = w < G && slice_is_giant(span, adj, f1 - f0);
+    const uint32_t np = gi ? (uint32_t)((span + P - 1) / P) : 0u;
+    uint32_t inc = np;  // inclusive scan over the 64 lanes
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)inc, sft);
+      inc += lane >= (uint32_t)sft ? o : 0u;
+    }
+    if (w <= G) pre[w] = carry + inc - np;
+    carry += (uint32_t)__shfl((int)inc, 63);
+  }
+  if (lane == 0) pre[G] = carry;
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t NP = carry;
+  const uint32_t T = G * kStageW * 64u;
+  const uint32_t t0 = (blockIdx.x * kStageW + (threadIdx.x >> 6)) * 64u + lane;
+  uint32_t* acc = scratch;
+  uint32_t* cnt = scratch + (kGiantPieces + 4096u);
+  uint32_t nsteps = 1;  // binary-search steps over a slice's per + 1 offsets
+  while ((1ull << nsteps) <= per) ++nsteps;
+
+  for (uint32_t pbase = 0; pbase < NP; pbase += T) {
+    const uint32_t p = pbase + t0;
+    const bool act = p < NP;
+    // the lane's giant slice g: the last g with pre[g] <= p
+    uint32_t g = 0;
+    for (uint32_t step = 256u; step > 0; step >>= 1)
+      if (g + step < G && pre[g + step] <= p) g += step;
+    const uint64_t F0 = (uint64_t)g * per < nframes ? (uint64_t)g * per : nframes;
+    const uint64_t F1 = F0 + per < nframes ? F0 + per : nframes;
+    const uint64_t S = off[F0], E = off[F1];
+    const uint64_t k = act ? p - pre[g] : 0;
+    const uint64_t a = act ? S + k * P : S, b = act ? (S + (k + 1) * P < E ? S + (k + 1) * P : E) : S;
+    const bool last_piece = act && b == E;
+    // lb = the first frame in [F0, F1] starting at or after a (wave-uniform step count)
+    uint64_t lo = F0, hi = F1;
+    for (uint32_t it = 0; it < nsteps + 1u; ++it) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const uint64_t om = off[mid];
+      const bool go = lo < hi;
+      lo = go && om < a ? mid + 1 : lo;
+      hi = go && !(om < a) ? mid : hi;
+    }
+    const uint64_t lb = lo;
+    const uint64_t olb = off[lb];
+    // the frame the piece starts in: one that began before a, or the first at a
+    const bool cross_in = lb > F0 && olb > a;
+    uint64_t cur = cross_in ? lb - 1 : lb;
+    uint64_t scur = cross_in ? off[lb - 1] : olb;
+    uint64_t x = cur < F1 ? off[cur + 1] : ~0ull;  // the current frame's end
+    uint32_t r = cross_in ? 0u : 0xFFFFFFFFu;
+    // a frame's end event (its end at `at`): finish it here when all of it lies
+    // in the piece, else add this piece's part
+    auto frame_end = [&](bool ev, uint64_t at) {
+      const bool here = scur >= a && at <= b;
+      if (ev && here) stage_store<MODE>(out, cur, stage_value<MODE>(r, at - scur));
+      if (ev && !here) {
+        const uint32_t slot = pre[g] + (uint32_t)((scur - S) / P) + 1u;
+        const uint32_t nparts = (uint32_t)((at - 1u - S) / P - (scur - S) / P + 1u);
+        __hip_atomic_fetch_xor(acc + slot, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1u == nparts) {
+          const uint32_t tot = __hip_atomic_exchange(acc + slot, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          stage_store<MODE>(out, cur, stage_value<MODE>(tot, at - scur));
+        }
+      }
+    };
+    auto advance = [&](bool ev) {
+      const uint64_t nx = off[cur + 2u <= F1 ? cur + 2u : F1];  // (loaded by every lane)
+      cur = ev ? cur + 1u : cur;
+      scur = ev ? x : scur;
+      r = ev ? 0xFFFFFFFFu : r;
+      x = ev ? (cur < F1 ? nx : ~0ull) : x;
+    };
+    // 128-byte blocks from the line holding a
+    const uint64_t blk0 = a - ((reinterpret_cast<uintptr_t>(bytes) + a) & 127u);
+    uint32_t nblk = act ? (uint32_t)((b - blk0 + 127u) / 128u) : 0u;
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)nblk, sft);
+      nblk = o > nblk ? o : nblk;
+    }
+    nblk = (uint32_t)__builtin_amdgcn_readfirstlane((int)nblk);
+    for (uint32_t t = 0; t < nblk; ++t) {
+      const uint64_t bp = blk0 + 128ull * t;
+      const bool inb = act && bp < b;
+      // (a line that holds a byte of the buffer is mapped: lanes past their
+      // piece re-read the line holding a)
+      const u32x4* src = reinterpret_cast<const u32x4*>(bytes + (inb ? bp : blk0));
+      u32x4 w[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) w[m] = src[m];
+      const bool clean = !inb || (bp >= a && bp + 128u <= b && x >= bp + 128u);
+      if (__builtin_amdgcn_ballot_w64(!clean) == 0) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const uint32_t nr = s_z8unit(lds, r ^ w[u >> 1][(2 * u) & 3], w[u >> 1][(2 * u + 1) & 3], z8);
+          r = inb ? nr : r;
+        }
+        continue;
+      }
+      // byte by byte, from the lane's 128 bytes staged in LDS
+#pragma unroll
+      for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 128u * lane + 16u * m) = w[m];
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = 0; i < 128u; ++i) {
+        const uint64_t pos = bp + i;
+        const bool live = inb && pos >= a && pos < b;
+        while (__builtin_amdgcn_ballot_w64(live && x == pos) != 0) {
+          const bool ev = live && x == pos;
+          frame_end(ev, pos);
+          advance(ev);
+        }
+        const uint32_t byte = (uint32_t)(uint8_t)tr[128u * lane + i];
+        const uint32_t nr = s_z1(lds, r ^ byte, b0);
+        r = live ? nr : r;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // the piece end b: the frame ending exactly there finishes; one that runs
+    // on adds Z_{x - b}(r); the last piece also finishes the empty frames at E
+    const bool endb = act && cur < F1 && x == b;
+    frame_end(endb, b);
+    advance(endb && last_piece);  // (frames starting at b belong to the next piece)
+    while (__builtin_amdgcn_ballot_w64(last_piece && cur < F1 && x == b) != 0) {
+      const bool ev = last_piece && cur < F1 && x == b;
+      frame_end(ev, b);
+      advance(ev);
+    }
+    const bool runs_on = act && !endb && cur < F1 && x > b && x != ~0ull;
+    const uint32_t z = s_zd64(lds, image, runs_on ? x - b : 0u, r);
+    r = runs_on ? z : r;
+    frame_end(runs_on, x);
+  }
+}
+
+// ---------------------------------------------------------------- the kernel
+template <StageMode MODE>
+__global__ void __launch_bounds__(kStageW * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
-                   uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out) {
-  using LY = StageLds<W, BF, DEFER ? 3u * 4096u : PATCH == 2 ? 4u * 4096u : 0u>;
-  static_assert(!DEFER || FOLD == 8, "the deferred correction runs on the slicing-by-8 fold");
-  static_assert(PATCH == 0 || (FOLD == 8 && !DEFER), "the patched boundary word runs on the slicing-by-8 fold");
-  constexpr uint32_t kLast = BF + 1;  // the list's last entry (a sentinel past bf)
-  constexpr uint32_t kThreads = W * 64;
-  __shared__ __attribute__((aligned(16))) char lds[LY::kBytes];
-  // ---- image: A / B values expanded into their 32 bank columns (FOLD 4: the
-  // Z_4 values into 16), nibble tables verbatim
+                   uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out,
+                   uint32_t policy, uint32_t* __restrict__ scratch) {
+  constexpr uint32_t kLast = kStageBF + 1;  // the list's last entry (a sentinel past bf)
+  constexpr uint32_t kThreads = kStageW * 64;
+  __shared__ __attribute__((aligned(16))) char lds[kSBytes];
+  const uint64_t fb0 = (uint64_t)blockIdx.x * frames_per_wg < nframes ? (uint64_t)blockIdx.x * frames_per_wg : nframes;
+  const uint64_t fb1 = fb0 + frames_per_wg < nframes ? fb0 + frames_per_wg : nframes;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  // ---- this workgroup's slice, and whether the launch has giant slices
+  // (every workgroup reads the G + 1 slice bounds: L2 hits after the first)
+  const uint32_t own = slice_kind(bytes, off, fb0, fb1, policy);
+  bool giant = false;
+  for (uint32_t w0 = 0; w0 < gridDim.x; w0 += 64u) {
+    const uint32_t w = w0 + lane;
+    const uint64_t f0 = (uint64_t)w * frames_per_wg < nframes ? (uint64_t)w * frames_per_wg : nframes;
+    const uint64_t f1 = f0 + frames_per_wg < nframes ? f0 + frames_per_wg : nframes;
+    const uint64_t s = off[f0], e = off[f1];
+    const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
+    giant = giant || __builtin_amdgcn_ballot_w64(w < gridDim.x && slice_is_giant(span, adj, f1 - f0)) != 0;
+  }
+  if (own != kSliceStage && !giant) return;
+  // ---- image: the T8 values expanded into their 8 bank columns, the nibble tables verbatim
   {
     const uint32_t t = threadIdx.x;
-    if constexpr (FOLD == 8) {
-      for (uint32_t vi = t; vi < 2048u; vi += kThreads) {
-        const uint32_t v = image[kStageZ8Img + vi];
-        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 5));
-        const uint4 v4 = {v, v, v, v};
-        row[0] = v4;
-        row[1] = v4;
-      }
-    } else if constexpr (FOLD == 4) {
-      for (uint32_t vi = t; vi < 1024u; vi += kThreads) {
-        const uint32_t v = image[kStageZ4Img + vi];
-        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 6));
-        const uint4 v4 = {v, v, v, v};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) row[(i + vi) & 3u] = v4;
-      }
-    } else {
-      for (uint32_t vi = t; vi < 512u; vi += kThreads) {
-        const uint32_t v = image[vi];
-        const uint32_t m = vi >> 8, e = vi & 255u;
-        uint4* row = reinterpret_cast<uint4*>(lds + kSTab + (e << 8) + (m << 7));
-        const uint4 v4 = {v, v, v, v};
-#pragma unroll
-        for (int i = 0; i < 8; ++i) row[(i + vi) & 7u] = v4;
-      }
+    for (uint32_t vi = t; vi < 2048u; vi += kThreads) {
+      const uint32_t v = image[kStageZ8Img + vi];
+      uint4* row = reinterpret_cast<uint4*>(lds + kSTab + ((vi & 255u) << 8) + ((vi >> 8) << 5));
+      const uint4 v4 = {v, v, v, v};
+      row[0] = v4;
+      row[1] = v4;
     }
-    if constexpr (LY::kNibInLds)
-      for (uint32_t i = t; i < 31u * 128u; i += kThreads)
-        reinterpret_cast<uint32_t*>(lds + LY::kNib)[i] = image[512 + i];
-    if constexpr (LY::kZxBytes != 0)
-      for (uint32_t i = t; i < LY::kZxBytes / 4u; i += kThreads)
-        reinterpret_cast<uint32_t*>(lds + LY::kZx)[i] = image[(DEFER ? kStageZxImg : kStageZyImg) + i];
-    if (t == 0) *reinterpret_cast<uint32_t*>(lds + LY::kCtr) = 0;
+    for (uint32_t i = t; i < 31u * 128u; i += kThreads) reinterpret_cast<uint32_t*>(lds + kSNib)[i] = image[512 + i];
+    if (t == 0) *reinterpret_cast<uint32_t*>(lds + kSCtr) = 0;
   }
   __syncthreads();
-  const uint64_t fb0 = (uint64_t)blockIdx.x * frames_per_wg;
-  if (fb0 >= nframes) return;
-  const uint64_t fb1 = fb0 + frames_per_wg < nframes ? fb0 + frames_per_wg : nframes;
-  const uint32_t nslice = (uint32_t)(fb1 - fb0);
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t b0 = (lane & (FOLD == 8 ? 7u : FOLD == 4 ? 15u : 31u)) << 2;
+  const uint32_t b0 = (lane & 7u) << 2;
   const Z8Lane z8(lane);
-  const Z4Lane zl(lane);
-  char* tr = lds + LY::kTr + 8192u * wv;
-  uint32_t* list = reinterpret_cast<uint32_t*>(lds + LY::kBnd + LY::kList * wv);
+  char* tr = lds + kSTr + 8192u * wv;
+  uint32_t* list = reinterpret_cast<uint32_t*>(lds + kSBnd + kSList * wv);
+  const uint32_t nslice = (uint32_t)(fb1 - fb0);
   constexpr uint32_t elem = MODE == StageMode::kCrc ? 4u : 1u;
   const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<char*>(out) + fb0 * elem, (short)0, (int)(nslice * elem), 0x00020000);
@@ -276,108 +449,46 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 
   auto grab = [&]() -> uint32_t {
     uint32_t b = 0;
-    if (lane == 0) b = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + LY::kCtr), 1u, __ATOMIC_RELAXED,
+    if (lane == 0) b = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(lds + kSCtr), 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
   };
-  // PF (variants 322 / 323): the next block's offsets (its boundary list, A
-  // and E among them) are loaded while this block folds.  The loads are inline
-  // asm, so hipcc neither waits for them early nor counts them; the ring's
-  // vmcnt(0) at the block end (and once before the first block) makes them
-  // ready, and that asm names them as operands, so no use moves above it.
-  // They are older than every ring operation, so the ring's static vmcnt(10)
-  // still covers its slot.
-  constexpr bool PF = PATCH == 3;
-  constexpr uint32_t kNL = (BF + 2) / 64;
-  static_assert(!PF || kNL == 6, "the prefetch asm names six offsets per lane");
-  uint64_t pre[6] = {0, 0, 0, 0, 0, 0};
-  auto prefetch = [&](uint32_t b) {
-    const uint64_t fr = (uint64_t)b * BF;
-    const uint32_t bfx = fr < nslice ? (uint32_t)(nslice - fr < BF ? nslice - fr : BF) : 0u;
-    const uint64_t* p0 = off + fb0 + (fr < nslice ? fr : 0u);  // (past the slice: entry fb0, a valid address)
-#pragma unroll
-    for (uint32_t i = 0; i < 6; ++i) {
-      const uint32_t jj = lane + 64u * i;
-      const uint64_t* p = p0 + (jj <= bfx ? jj : bfx);
-      asm volatile("global_load_dwordx2 %0, %1, off" : "=&v"(pre[i]) : "v"(p));
-    }
-  };
-  auto pre_ready = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(pre[0]), "+v"(pre[1]), "+v"(pre[2]), "+v"(pre[3]), "+v"(pre[4]), "+v"(pre[5]));
-  };
-  uint32_t blk_pf = 0;
-  if constexpr (PF) {
-    blk_pf = grab();
-    prefetch(blk_pf);
-    pre_ready();
-  }
 
   for (;;) {
-    const uint32_t blk = PF ? blk_pf : grab();
-    const uint64_t f0r = (uint64_t)blk * BF;  // relative to fb0
+    if (own != kSliceStage) break;
+    const uint32_t blk = grab();
+    const uint64_t f0r = (uint64_t)blk * kStageBF;  // relative to fb0
     if (f0r >= nslice) break;
-    const uint32_t bf = (uint32_t)(nslice - f0r < BF ? nslice - f0r : BF);
+    const uint32_t bf = (uint32_t)(nslice - f0r < kStageBF ? nslice - f0r : kStageBF);
     const uint64_t f0 = fb0 + f0r;
-    uint64_t A, E;
-    if constexpr (PF) {
-      uint64_t ev = pre[0];
-#pragma unroll
-      for (uint32_t i = 1; i < 6; ++i) ev = (bf >> 6) == i ? pre[i] : ev;
-      const uint32_t el = bf & 63u;
-      A = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pre[0], 0) |
-          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pre[0] >> 32), 0) << 32);
-      E = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ev, (int)el) |
-          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ev >> 32), (int)el) << 32);
-    } else {
-      A = off[f0], E = off[f0 + bf];
-    }
+    const uint64_t A = off[f0], E = off[f0 + bf];
     const uint8_t* pa = bytes + A;
     const uint32_t adj = (uint32_t)(reinterpret_cast<uintptr_t>(pa) & 127u);
-    const uint64_t span = E > A ? E - A + adj : adj;
-    // ---- boundary list (relative to the line-aligned base): x_j = off[f0 + j] - A + adj
+    // ---- boundary list (relative to the line-aligned base): x_j = off[f0 + j] - A + adj;
+    // a block whose offsets are out of order (an entry outside [A, E] or below
+    // its predecessor) is folded one lane per frame instead
+    bool ooo = E < A;
 #pragma unroll
-    for (uint32_t i = 0; i < (BF + 2) / 64; ++i) {  // (whole-wave loads: entry j > bf re-reads entry bf)
+    for (uint32_t i = 0; i < (kStageBF + 2) / 64; ++i) {  // (whole-wave loads: entry j > bf re-reads entry bf)
       const uint32_t j = lane + 64u * i;
-      const uint64_t o = PF ? pre[i] : off[f0 + (j <= bf ? j : bf)];
-      const uint32_t x = o > A ? (uint32_t)(o - A) + adj : adj;  // (non-decreasing offsets: o >= A)
+      const uint64_t o = off[f0 + (j <= bf ? j : bf)];
+      ooo = ooo || o < A || o > E;
+      const uint32_t x = o > A ? (uint32_t)(o - A) + adj : adj;
       list[j] = j <= bf ? x : kSNone;
     }
-    if constexpr (PF) {
-      blk_pf = grab();
-      prefetch(blk_pf);
-    }
     __builtin_amdgcn_wave_barrier();
-    if (span >= (1ull << 31) - 65536) {
-      // gigabyte frames: byte-serial fold per frame, one lane per frame
-      // (the byte loop runs with the whole wave active: a lane past its frame
-      // re-reads byte A and keeps its register, so no load issues under
-      // narrowed exec — the audit's loop rule)
-      for (uint32_t j0 = 0; j0 < bf; j0 += 64u) {
-        const uint32_t j = j0 + lane;
-        uint32_t r = 0xFFFFFFFFu;
-        const uint64_t s = j < bf ? off[f0 + j] : A, e0 = j < bf ? off[f0 + j + 1] : A;
-        const uint64_t e = e0 > s ? e0 : s;
-        for (uint64_t q = s;; ++q) {
-          const bool act = q < e;
-          if (__builtin_amdgcn_ballot_w64(act) == 0) break;
-          const uint32_t b = bytes[act ? q : A];
-          const uint32_t nr = s_z1<FOLD>(lds, r ^ b, b0);
-          r = act ? nr : r;
-        }
-        if (j < bf) {
-          const uint32_t crc = ~r;
-          const uint32_t v = MODE == StageMode::kCrc ? crc : (uint32_t)(e - s >= 4 && crc == 0x2144DF1Cu);
-          if (MODE == StageMode::kCrc)
-            __builtin_amdgcn_raw_buffer_store_b32(v, out_rsrc, (uint32_t)(f0r + j) * 4u, 0, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, (uint32_t)(f0r + j), 0, 0);
-        }
-      }
-      if constexpr (PF) pre_ready();
+#pragma unroll
+    for (uint32_t i = 0; i < (kStageBF + 2) / 64; ++i) {
+      const uint32_t j = lane + 64u * i;
+      ooo = ooo || (j >= 1u && j <= bf && list[j] < list[j - 1u]);
+    }
+    if (__builtin_amdgcn_ballot_w64(ooo) != 0) {
+      ooo_block<MODE>(lds, bytes, off, f0, bf, out, lane, b0);
+      __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next block
       continue;
     }
-    const uint32_t sp = (uint32_t)span;
+    // (span < 2^31 - 2^20: the slice is not giant, dispatch.hpp)
+    const uint32_t sp = (uint32_t)(E - A) + adj;
     // 64 Q > sp: the block's last boundary (at sp) must lie inside a stretch
     uint32_t Q = ((sp + 64u) / 64u + 127u) & ~127u;
     Q = Q < 128u ? 128u : Q;
@@ -437,12 +548,6 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
                      ::"v"(hv0), "v"(hf0), "v"(hv1), "v"(hf1), "s"(out_rsrc) : "memory");
       hf0 = hf1 = kSOOB;
     };
-    // the block's first two rounds go out before the boundary search
-    u32x4 buf0[8], buf1[8];
-    flush();  // (two stores, so that the first waits count alike)
-    issue(buf0, 0);
-    flush();
-    issue(buf1, 1);
     // ---- this lane's stretch [Sk, Sk + Q) and its first boundary j = lower_bound(list, Sk)
     const uint32_t Sk = lane * Q;
     uint32_t lo = 0, hi = bf + 1u;
@@ -503,9 +608,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       asm volatile("s_waitcnt vmcnt(10)"
                    : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
                      "+v"(cur[6]), "+v"(cur[7]));
-      if constexpr (PATCH != 4)  // (variant 328, timing only: the lines read back stale)
 #pragma unroll
-        for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
+      for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 1024 * m + 16u * lane) = cur[m];
       flush();
       issue(cur, rr + 2u);
       // the lane's whole line in one LDS round trip (both halves)
@@ -533,195 +637,79 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
               r = ev ? 0xFFFFFFFFu : r;
               advance(ev);
             }
-            r = s_z1<FOLD>(lds, r ^ ((w >> (8u * (b & 3u))) & 0xFFu), b0);  // (one byte: Z_1 shifts r, not w)
+            r = s_z1(lds, r ^ ((w >> (8u * (b & 3u))) & 0xFFu), b0);  // (one byte: Z_1 shifts r, not w)
           }
           continue;
         }
         const uint32_t kb = in ? rel >> 2 : 99u, c = rel & 3u;
         const uint32_t lm = in ? (uint32_t)((1ull << (8u * c)) - 1ull) : 0u;
         const uint32_t Kc = c == 0u ? 0xFFFFFFFFu : c == 1u ? kK1 : c == 2u ? kK2 : kK3;
-        uint32_t ecap = 0;
-        if constexpr (DEFER) {
-          // no boundary selects in the fold: the plain fold, one capture of r
-          // per 8-byte unit, and the boundary's effect added after the half
-          // (r_true = r_plain ^ Z_{64 - 4d}(e ^ K_c))
-          uint32_t rc = 0;
-          const uint32_t ub = kb >> 1;
+        // the boundary word patched once per half, read back from the staged
+        // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
+        // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
+        // = 0 drops r), so a unit costs one compare and two selects
+        const uint32_t ub = (kb >> 1) & 7u;
+        const bool odd = (kb & 1u) != 0u;
+        const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (ub >> 1) + rot) & 7u) +
+                                                         8u * (ub & 1u));
+        const uint32_t wb = __builtin_amdgcn_bitop3_b32(odd ? wp.y : wp.x, lm, Kc, 0x9A);
+        const uint32_t wb0 = odd ? 0u : wb;
+        const uint32_t kbu = kb >> 1;  // (49 in a lane without a boundary)
+        uint32_t rc = 0;
 #pragma unroll
-          for (uint32_t u = 0; u < 8; ++u) {
-            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
-            rc = ub == u ? r : rc;
-            r = s_z8half(lds, r ^ w0, z8, 0) ^ s_z8half(lds, w1, z8, 1);
-          }
-          if (__builtin_amdgcn_ballot_w64(in) != 0) {
-            // the boundary unit's two words, from the staged line
-            const uint32_t u = (kb >> 1) & 7u;
-            const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (u >> 1) + rot) & 7u) +
-                                                             8u * (u & 1u));
-            const bool odd = kb & 1u;
-            const uint32_t z4 = s_z8half(lds, rc ^ wp.x, z8, 1);  // the state before w1
-            const uint32_t rd = odd ? z4 : rc;
-            ecap = rd ^ ((odd ? wp.y : wp.x) & lm);
-            // Z_{4m}(ecap ^ K_c), m = 16 - kb dwords, by binary powers: Z_4, Z_8
-            // (the fold's tables), Z_16 / Z_32 / Z_64 (the shared tables)
-            const uint32_t m = 16u - (kb & 15u);
-            uint32_t z = ecap ^ Kc;
-            z = (m & 1u) ? s_z8half(lds, z, z8, 1) : z;
-            z = (m & 2u) ? s_z8half(lds, z, z8, 0) : z;
-#pragma unroll
-            for (uint32_t t = 0; t < 3; ++t) {
-              const uint32_t* zt = reinterpret_cast<const uint32_t*>(lds + LY::kZx) + 1024u * t;
-              const uint32_t zz = __builtin_amdgcn_bitop3_b32(zt[z & 0xFFu], zt[256u + ((z >> 8) & 0xFFu)],
-                                                              zt[512u + ((z >> 16) & 0xFFu)], 0x96) ^
-                                  zt[768u + (z >> 24)];
-              z = (m & (4u << t)) ? zz : z;
-            }
-            r = in ? r ^ z : r;
-          }
-        } else if constexpr (PATCH == 2) {
-          // the patched boundary word, and the half as two chains of four
-          // units: A from r, B from 0 (independent: two LDS round trips in
-          // flight per lane); after the half r = Z_32(A) ^ B, or B alone when
-          // the boundary lies in B.  A boundary in B captured B's local state:
-          // the true one adds Z_{8(u-4)}(A), read with Z_32(A) in one round
-          // trip from the shared Z_8 / Z_16 / Z_24 / Z_32 tables
-          const uint32_t ub = (kb >> 1) & 7u;
-          const bool odd = (kb & 1u) != 0u;
-          const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (ub >> 1) + rot) & 7u) +
-                                                           8u * (ub & 1u));
-          const uint32_t wb = __builtin_amdgcn_bitop3_b32(odd ? wp.y : wp.x, lm, Kc, 0x9A);
-          const uint32_t wb0 = odd ? 0u : wb;
-          const uint32_t kbu = kb >> 1;  // (49 in a lane without a boundary)
-          uint32_t ra = r, rbv = 0, rc = 0;
-#pragma unroll
-          for (uint32_t u = 0; u < 4; ++u) {
-            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
-            const uint32_t x0 = q[2 + (u >> 1)][(2u * u) & 3u], x1w = q[2 + (u >> 1)][(2u * u + 1u) & 3u];
-            const bool au = kbu == u, a1 = au && odd;
-            const bool bu = kbu == u + 4u, b1 = bu && odd;
-            rc = au ? ra : bu ? rbv : rc;
-            ra = s_z8unit(lds, au ? wb0 : ra ^ w0, a1 ? wb : w1, z8);
-            rbv = s_z8unit(lds, bu ? wb0 : rbv ^ x0, b1 ? wb : x1w, z8);
-          }
-          const bool inb = kbu - 4u < 4u;
-          const uint32_t* zy = reinterpret_cast<const uint32_t*>(lds + LY::kZx);
-          const uint32_t zsel = 1024u * ((kbu - 5u) & 3u);  // Z_{8(u-4)} for u = 5..7
-          uint32_t a32[4], ac[4];
-#pragma unroll
-          for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t e = (ra >> (8u * k)) & 0xFFu;
-            a32[k] = zy[3u * 1024u + 256u * k + e];
-            ac[k] = zy[zsel + 256u * k + e];
-          }
-          const uint32_t z32 = __builtin_amdgcn_bitop3_b32(a32[0], a32[1], a32[2], 0x96) ^ a32[3];
-          const uint32_t zc = __builtin_amdgcn_bitop3_b32(ac[0], ac[1], ac[2], 0x96) ^ ac[3];
-          r = inb ? rbv : z32 ^ rbv;
-          const uint32_t rct = inb ? rc ^ (kbu == 4u ? ra : zc) : rc;
-          const uint32_t z4t = s_z8half(lds, rct ^ wp.x, z8, 1);
-          ecap = odd ? z4t ^ (wp.y & lm) : rct ^ (wp.x & lm);
-        } else if constexpr (PATCH == 1 || PATCH >= 3) {
-          // the boundary word patched once per half, read back from the staged
-          // line: (w & ~lm) ^ K_c; the boundary unit u = kb >> 1 then enters
-          // (patch, w1) for a boundary in w0 and (0, patch) for one in w1 (Z_8(0)
-          // = 0 drops r), so a unit costs one compare and two selects
-          const uint32_t ub = (kb >> 1) & 7u;
-          const bool odd = (kb & 1u) != 0u;
-          const uint2 wp = *reinterpret_cast<const uint2*>(tr + rb + 16u * ((4u * h + (ub >> 1) + rot) & 7u) +
-                                                           8u * (ub & 1u));
-          const uint32_t wb = __builtin_amdgcn_bitop3_b32(odd ? wp.y : wp.x, lm, Kc, 0x9A);
-          const uint32_t wb0 = odd ? 0u : wb;
-          const uint32_t kbu = kb >> 1;  // (49 in a lane without a boundary)
-          uint32_t rc = 0;
-#pragma unroll
-          for (uint32_t u = 0; u < 8; ++u) {
-            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
-            const bool au = kbu == u, a1 = au && odd;
-            rc = au ? r : rc;
-            if constexpr (PATCH == 5)  // (variant 330, timing only: a two-op stand-in for the unit's lookups)
-              r = __builtin_amdgcn_alignbit(au ? wb0 : r ^ w0, a1 ? wb : w1, 7) ^ (a1 ? wb : w1);
-            else
-              r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
-          }
-          // (variant 332, timing only: the ending frame's capture and Z_c skipped)
-          const uint32_t z4t = PATCH == 6 ? rc : s_z8half(lds, rc ^ wp.x, z8, 1);
-          ecap = odd ? z4t ^ (wp.y & lm) : rc ^ (wp.x & lm);
-        } else if constexpr (FOLD == 8) {
-          // 8-byte units; the unit holding the boundary captures (r, w0, w1)
-          uint32_t rc = 0, w0c = 0, w1c = 0;
-#pragma unroll
-          for (uint32_t u = 0; u < 8; ++u) {
-            const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
-            const bool a0 = 2u * u == kb, a1 = 2u * u + 1u == kb, au = a0 || a1;
-            rc = au ? r : rc, w0c = au ? w0 : w0c, w1c = au ? w1 : w1c;
-            const uint32_t v0 = a0 ? __builtin_amdgcn_bitop3_b32(w0, lm, Kc, 0x9A) : r ^ w0;
-            const uint32_t v1 = a1 ? __builtin_amdgcn_bitop3_b32(w1, lm, Kc, 0x9A) : w1;
-            const uint32_t yw = s_z8half(lds, v1, z8, 1);  // Z_4(v1): off the chain
-            const uint32_t yr = s_z8half(lds, v0, z8, 0);
-            r = (a1 ? 0u : yr) ^ yw;  // a new frame in w1 owes nothing to r
-          }
-          // the ending frame's state before Z_c: in w0, r ^ (w0 & lm); in w1,
-          // Z_4(r ^ w0) ^ (w1 & lm) (Z_4 = the T8_4..7 half)
-          const uint32_t z4t = s_z8half(lds, rc ^ w0c, z8, 1);
-          ecap = (kb & 1u) ? z4t ^ (w1c & lm) : rc ^ (w0c & lm);
-        } else {
-#pragma unroll
-          for (uint32_t d = 0; d < 16; ++d) {
-            const uint32_t w = q[d >> 2][d & 3u];
-            const bool at = d == kb;
-            ecap = at ? __builtin_amdgcn_bitop3_b32(r, w, lm, 0x78) : ecap;    // r ^ (w & lm)
-            const uint32_t vr = __builtin_amdgcn_bitop3_b32(w, lm, Kc, 0x9A);  // (w & ~lm) ^ Kc
-            const uint32_t v = at ? vr : r ^ w;
-            r = s_z4<FOLD>(lds, v, b0, zl);
-          }
+        for (uint32_t u = 0; u < 8; ++u) {
+          const uint32_t w0 = q[u >> 1][(2u * u) & 3u], w1 = q[u >> 1][(2u * u + 1u) & 3u];
+          const bool au = kbu == u, a1 = au && odd;
+          rc = au ? r : rc;
+          r = s_z8unit(lds, au ? wb0 : r ^ w0, a1 ? wb : w1, z8);
         }
+        const uint32_t z4t = s_z8half(lds, rc ^ wp.x, z8, 1);
+        const uint32_t ecap = odd ? z4t ^ (wp.y & lm) : rc ^ (wp.x & lm);
         if (__builtin_amdgcn_ballot_w64(in) != 0) {
-          uint32_t S = ecap;  // Z_c(e), c = 0..3
-          if constexpr (PATCH == 6) {
-          } else if constexpr (FOLD == 8) {
-            // Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e) = ... T8_{8-c+i}[byte i]
-            uint32_t y[3];
+          // Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e) = ... T8_{8-c+i}[byte i]
+          uint32_t y[3];
 #pragma unroll
-            for (uint32_t i = 0; i < 3; ++i)
-              y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(ecap, b0, 0x0c020400u + (i << 8)) +
-                                    (((8u - c + i) & 7u) << 5));
-            const uint32_t sh = c == 0u ? ecap : ecap >> (8u * c);
-            S = __builtin_amdgcn_bitop3_b32(sh, c > 0u ? y[0] : 0u, c > 1u ? y[1] : 0u, 0x96) ^ (c > 2u ? y[2] : 0u);
-          } else if constexpr (FOLD == 4) {
-            // one round trip: Z_c(e) = (e >> 8c) ^ XOR_{i<c} Z_{c-i}(byte i of e),
-            // Z_m(b) = Z_4(b << 8 (4 - m)) = table 4 - m's entry b
-            uint32_t y[3];
-#pragma unroll
-            for (uint32_t i = 0; i < 3; ++i)
-              y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(ecap, b0, 0x0c020400u + (i << 8)) +
-                                    (((4u - c + i) & 3u) << 6));
-            const uint32_t sh = c == 0u ? ecap : ecap >> (8u * c);
-            S = __builtin_amdgcn_bitop3_b32(sh, c > 0u ? y[0] : 0u, c > 1u ? y[1] : 0u, 0x96) ^ (c > 2u ? y[2] : 0u);
-          } else {
-#pragma unroll
-            for (uint32_t s = 0; s < 3; ++s) {
-              const uint32_t z = s_z1<FOLD>(lds, S, b0);
-              S = s < c ? z : S;
-            }
-          }
+          for (uint32_t i = 0; i < 3; ++i)
+            y[i] = s_lds(lds, kSTab + __builtin_amdgcn_perm(ecap, b0, 0x0c020400u + (i << 8)) +
+                                  (((8u - c + i) & 7u) << 5));
+          const uint32_t sh = c == 0u ? ecap : ecap >> (8u * c);
+          const uint32_t S = __builtin_amdgcn_bitop3_b32(sh, c > 0u ? y[0] : 0u, c > 1u ? y[1] : 0u, 0x96) ^
+                             (c > 2u ? y[2] : 0u);
           end_at(in, S, x, (int)h);
           advance(in);
         }
       }
     };
+    // the block's first two rounds, then a drain before the ring loop: hipcc
+    // gives the loop's ring registers other homes than these issues' outputs
+    // and copies them over in the loop preheader, which must not happen while
+    // the loads are in flight (tools/prof/audit_ring.py; the round-4 build
+    // happened to coalesce them).  Both rounds' loads leave back to back, so
+    // waiting for the second as well costs little more than waiting for the
+    // first, which round 0 does anyway.
+    u32x4 buf0[8], buf1[8];
+    flush();  // (two stores, so that the first waits count alike)
+    issue(buf0, 0);
+    flush();
+    issue(buf1, 1);
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(buf0[0]), "+v"(buf0[1]), "+v"(buf0[2]), "+v"(buf0[3]), "+v"(buf0[4]), "+v"(buf0[5]),
+                   "+v"(buf0[6]), "+v"(buf0[7]), "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]),
+                   "+v"(buf1[4]), "+v"(buf1[5]), "+v"(buf1[6]), "+v"(buf1[7]));
     for (uint32_t rr = 0; rr < rounds; rr += 2) {
       round_step(buf0, rr);
       if (rr + 1u < rounds) round_step(buf1, rr + 1u);
+      if (rr + 2u >= rounds)  // the last round: drain the ring inside the loop (the exit's copies come after it)
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(buf0[0]), "+v"(buf0[1]), "+v"(buf0[2]), "+v"(buf0[3]), "+v"(buf0[4]), "+v"(buf0[5]),
+                       "+v"(buf0[6]), "+v"(buf0[7]), "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]),
+                       "+v"(buf1[4]), "+v"(buf1[5]), "+v"(buf1[6]), "+v"(buf1[7]));
     }
     flush();
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(buf0[0]), "+v"(buf0[1]), "+v"(buf0[2]), "+v"(buf0[3]), "+v"(buf0[4]),
                  "+v"(buf0[5]), "+v"(buf0[6]), "+v"(buf0[7]));
-    if constexpr (PF) asm volatile("" : "+v"(pre[0]), "+v"(pre[1]), "+v"(pre[2]), "+v"(pre[3]), "+v"(pre[4]), "+v"(pre[5]));
     asm volatile("" : "+v"(buf1[0]), "+v"(buf1[1]), "+v"(buf1[2]), "+v"(buf1[3]), "+v"(buf1[4]), "+v"(buf1[5]),
                  "+v"(buf1[6]), "+v"(buf1[7]));
-    if constexpr (PATCH == 7) {  // (variant 334, timing only: no carries)
-      __builtin_amdgcn_wave_barrier();
-      continue;
-    }
     // ---- carries: the true register at each stretch's start
     const uint32_t E1 = r;
     const bool hb = j > jstart;  // this stretch holds a boundary
@@ -738,7 +726,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       // stretches without a boundary (Jacobi sweeps until nothing changes)
       for (uint32_t it = 0; it < 64u; ++it) {
         const uint32_t Pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)up, (int)Pk);
-        const uint32_t zq = s_zd<LY>(lds, image, hbp ? 0u : Q, Pp);
+        const uint32_t zq = s_zd(lds, hbp ? 0u : Q, Pp);
         const uint32_t Pn = hbp ? Ep : zq ^ Ep;
         const bool ch = Pn != Pk;
         Pk = Pn;
@@ -746,7 +734,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       }
     }
     if (__builtin_amdgcn_ballot_w64(rec) != 0) {
-      const uint32_t S = rec_S ^ s_zd<LY>(lds, image, rec ? rec_d : 0u, Pk);
+      const uint32_t S = rec_S ^ s_zd(lds, rec ? rec_d : 0u, Pk);
       const uint32_t crc = ~S;
       const uint32_t fr = (uint32_t)f0r + rec_j - 1u;
       if constexpr (MODE == StageMode::kCrc) {
@@ -759,86 +747,21 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     }
     __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next block
   }
+  if (giant)
+    giant_pieces<MODE>(lds, image, bytes, off, nframes, frames_per_wg, out, scratch, tr, list, lane, b0, z8);
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              int fold, int waves, const void* image, int num_cus, hipStream_t stream,
-                              bool big_blocks) {
+                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const uint64_t bfl = big_blocks ? kStageBFBig : fold == 12 ? kStageBFSmall : fold == 13 ? kStageBFMid
-                                                                            : fold == 15 ? kStageBF510 : kStageBF;
-  uint64_t grid = (n + bfl - 1) / bfl;
-  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
-  const uint64_t per = (n + grid - 1) / grid;
+  const SlicePlan pl = slice_plan(n, num_cus);
   const uint32_t* img = static_cast<const uint32_t*>(image);
-#define LNX_STAGE(M, F, W, ...)                                                                             \
-  hipLaunchKernelGGL((crc32_stage_kernel<M, F, W, ##__VA_ARGS__>), dim3((unsigned)grid), dim3(W * 64), 0, stream, \
-                     bytes, off, n, per, img, out)
-#ifdef LNX_RESEARCH  // variants 300-303, 308, 309: both folds, 382- or 766-frame blocks
-  // (10 waves per workgroup, variants 304-307, measured no faster in round 4
-  // and no longer fit its registers once the whole line is read at once)
-  if (fold >= 17 && fold <= 20) {  // timing-only diagnostics of the product form (wrong results)
-    if (fold == 17) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 4);
-    else if (fold == 18) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 5);
-    else if (fold == 19) LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 6);
-    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 7);
-    return hipGetLastError();
-  }
-  if (fold == 16) {  // the product form with 6 waves (1.5 per SIMD): how much the second wave per SIMD buys
-    if (big_blocks) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 8, 6, kStageBF, false, 1);
-    else LNX_STAGE(StageMode::kCrc, 8, 6, kStageBF, false, 1);
-    return hipGetLastError();
-  }
-  if (waves != 8) return hipErrorInvalidValue;
-#define LNX_STAGE_W(M, F) LNX_STAGE(M, F, 8)
-  if (fold == 15) {  // the product form with 510-frame blocks
-    if (big_blocks) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF510, false, 1);
-    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF510, false, 1);
-  } else if (fold == 14) {  // the product form with the next block's offsets loaded ahead
-    if (big_blocks) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 3);
-    else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 3);
-  } else if (fold == 12 || fold == 13) {  // the product form (patched boundary word) with 190- / 254-frame blocks
-    if (big_blocks) return hipErrorInvalidValue;
-    if (fold == 12) {
-      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBFSmall, false, 1);
-      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBFSmall, false, 1);
-    } else {
-      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBFMid, false, 1);
-      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBFMid, false, 1);
-    }
-  } else if (fold == 10 || fold == 11) {  // the slicing-by-8 fold with the boundary word patched once per half (11: two chains per half)
-    if (big_blocks) return hipErrorInvalidValue;
-    if (fold == 11) {
-      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 2);
-      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 2);
-    } else {
-      if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 1);
-      else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 1);
-    }
-  } else if (fold == 9) {  // the slicing-by-8 fold with the deferred boundary correction
-    if (big_blocks) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, true); else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, true);
-  } else if (fold == 8) {
-    if (big_blocks) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 8, 8); else LNX_STAGE(StageMode::kCrc, 8, 8);
-  } else if (big_blocks) {
-    if (fold != 4 || waves != 8) return hipErrorInvalidValue;
-    if (verify) LNX_STAGE(StageMode::kVerify, 4, 8, kStageBFBig); else LNX_STAGE(StageMode::kCrc, 4, 8, kStageBFBig);
-  } else if (fold == 4) {
-    if (verify) { LNX_STAGE_W(StageMode::kVerify, 4); } else { LNX_STAGE_W(StageMode::kCrc, 4); }
-  } else {
-    if (verify) { LNX_STAGE_W(StageMode::kVerify, 2); } else { LNX_STAGE_W(StageMode::kCrc, 2); }
-  }
-#undef LNX_STAGE_W
-#else  // the product form only: the slicing-by-8 fold with the patched boundary word, 8 waves, 382-frame blocks
-  if (fold != 8 || waves != 8 || big_blocks) return hipErrorInvalidValue;
-  if (verify) LNX_STAGE(StageMode::kVerify, 8, 8, kStageBF, false, 1);
-  else LNX_STAGE(StageMode::kCrc, 8, 8, kStageBF, false, 1);
-#endif
-#undef LNX_STAGE
+  if (verify)
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3((unsigned)pl.grid), dim3(kStageW * 64), 0, stream,
+                       bytes, off, n, pl.per, img, out, policy, scratch);
+  else
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3((unsigned)pl.grid), dim3(kStageW * 64), 0, stream,
+                       bytes, off, n, pl.per, img, out, policy, scratch);
   return hipGetLastError();
 }
 

@@ -117,11 +117,14 @@ def test_product_library_holds_only_product_kernels():
                       "ingress_verify_kernel", "ingress_verify_kernel", "ring_segments_kernel",
                       "sum16_lines_kernel"], others  # ingress: filtered / unfiltered verdicts, TX generate
     stage = [k for k in ks if "crc32_stage_kernel" in k]
-    assert all(re.search(r"StageModeE\dELi8ELi8E", k) for k in stage), stage  # the product fold / wave count
+    assert all(re.search(r"crc32_stage_kernelILNS_9StageModeE\dEEEv", k) for k in stage), stage  # CRC / verify only
     research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
     if os.path.exists(research):
         rk = _kernels(research)
         assert set(ks) <= set(rk) and len(rk) > len(ks) + 40
+        # the round-4 staged variants live in stage_research.hip's namespace lnx::rs only
+        assert any("2rs21crc32_stage_rs_kernel" in k for k in rk)
+        assert not any("crc32_stage_rs_kernel" in k for k in ks)
 
 
 def test_product_library_reads_no_environment():

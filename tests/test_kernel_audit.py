@@ -38,8 +38,8 @@ def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path, build):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-@pytest.mark.parametrize("src", ["crc32_kernel", "stage_kernel", "sum16_kernel", "ingress_kernel", "search_kernel",
-                                 "rx_ring"])
+@pytest.mark.parametrize("src", ["crc32_kernel", "stage_kernel", "stage_research", "sum16_kernel", "ingress_kernel",
+                                 "search_kernel", "rx_ring"])
 @pytest.mark.parametrize("build", ["product", "research"])
 def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
     """tools/prof/audit_loops.py over every product kernel: no innermost loop
@@ -58,18 +58,22 @@ def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-def test_stage_kernel_passes_the_ring_audit(tmp_path):
-    """The staged lane streams (stage_kernel.hip, research build): each round's
-    hand-placed vmcnt(10) must cover the 8 loads of the slot it drains, with
-    the held-result stores (2 per round, in asm so hipcc cannot drop or move
-    them) and the next slot's 8 loads younger than it."""
-    path = os.path.join(ROOT, "lneto_amd", "csrc", "stage_kernel.hip")
+@pytest.mark.parametrize("src,nsyms", [("stage_kernel", 2), ("stage_research", 30)])
+def test_stage_kernel_passes_the_ring_audit(tmp_path, src, nsyms):
+    """The staged lane streams (stage_kernel.hip: the product CRC / verify
+    pair; stage_research.hip: the round-4 variants): each round's hand-placed
+    vmcnt(10) must cover the 8 loads of the slot it drains, with the
+    held-result stores (2 per round, in asm so hipcc cannot drop or move them)
+    and the next slot's 8 loads younger than it."""
+    path = os.path.join(ROOT, "lneto_amd", "csrc", src + ".hip")
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-c", "--save-temps", "-DLNX_RESEARCH",
                     "-o", str(tmp_path / "k.o"), path], cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
-    syms = re.findall(r"^(_ZN3lnx18crc32_stage_kernel\w+):", open(tmp_path / asm).read(), flags=re.M)
-    assert len(syms) == 28  # CRC / verify x (the three folds, + 766-frame blocks, + the deferred correction,
-    #                          + the patched boundary word, + two chains per half, + 190- / 254-frame blocks, + offsets loaded a block ahead, + 510-frame blocks, + 6 waves, + 4 timing-only diagnostics)
+    syms = re.findall(r"^(_ZN3lnx\w*crc32_stage_(?:rs_)?kernel\w+):", open(tmp_path / asm).read(), flags=re.M)
+    # research: CRC / verify x (the three folds, + 766-frame blocks, + the deferred correction, + the patched
+    # boundary word, + two chains per half, + 190- / 254-frame blocks, + offsets loaded a block ahead, + 510-frame
+    # blocks, + 6 waves, + 6 timing-only diagnostics)
+    assert len(syms) == nsyms, syms
     for sym in syms:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_ring.py"),
                             str(tmp_path / asm), sym], capture_output=True, text=True)

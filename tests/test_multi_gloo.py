@@ -89,7 +89,7 @@ def test_bench_world2_on_cpu_ranks():
     port = _free_port()
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
-                        "--gpus", "2", "--steps", "4", "--warmup", "1", "--prewarm-s", "0", "--event-every", "2"],
+                        "--gpus", "2", "--steps", "4", "--warmup", "1", "--prewarm-s", "0"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=root)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

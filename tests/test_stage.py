@@ -1,21 +1,35 @@
-"""Staged lane streams (lneto_amd/csrc/stage_kernel.hip) on the
+"""The staged lane streams (lneto_amd/csrc/stage_kernel.hip)
+and the round-5 dispatch behind the plain entries (dispatch.hpp, §3.10) on the
 GPU against the C oracle (Go hash/crc32 IEEE restated; the arithmetic of
-ethernet.CRC32, lneto ethernet/crc.go:19-21): the Zipf mix, every length
-0..700 at odd lead-ins (variants 300 / 302: the two folds), tiny and empty frames (the byte-serial halves),
-frames longer than a stretch (the carry chain), jumbo and gigantic frames,
-tiny batches, and FCS verify (variants 301 / 303) with one flipped byte per frame
-for a third of the frames.  The schedule's algebra is pinned on the host in
+ethernet.CRC32, lneto ethernet/crc.go:19-21).
+
+Product entries, each case run through both: "auto" = lnx_crc32_batch /
+lnx_fcs_verify_batch (rows and staged kernels, each slice's kernel picked on
+the device), "short" = the _ex forms with LNX_BATCH_SHORT_FRAMES (every slice
+that fits goes to the staged kernel).  Cases: the Zipf mix, every length
+0..700 at odd lead-ins, tiny and empty frames (the byte-serial halves), frames
+longer than a stretch (the carry chain), jumbo and 3 MiB frames, tiny batches,
+FCS verify with flipped bytes, offsets out of order, batches whose slices go
+to different kernels, configs[3]'s whole 16 M-frame batch (offsets past 2^31),
+and giant slices (a 2.2 GB frame among short ones: the byte pieces).
+
+The round-4 research forms (stage_research.hip, liblneto_amd_research.so)
+keep one parity test each.  The schedule's algebra is pinned on the host in
 tests/test_stage_algebra.py."""
 import ctypes
+import time
 
 import numpy as np
 import pytest
 
+MODES = ["auto", "short"]
+# research forms (stage_research.hip): slicing-by-2 / 16-column Z_4 / slicing-by-8 fold, 766-frame blocks,
+# deferred correction, patched boundary word (the product's fold), two chains per half, 190- / 254-frame
+# blocks, offsets a block ahead, 510-frame blocks, 6 waves; verify form = var + 1
+RESEARCH_VARS = [300, 302, 308, 310, 312, 314, 316, 318, 320, 322, 324, 326]
 
-CRC_VARS = [300, 302, 308, 310, 312, 314, 316, 318, 320, 322, 324, 326]  # slicing-by-2 / 16-column Z_4 / slicing-by-8 fold, 766-frame blocks, deferred correction, patched boundary word, two chains per half, 190- / 254-frame blocks, offsets a block ahead, 510-frame blocks, 6 waves
 
-
-def _lib():
+def _research():
     import lneto_amd as L
     f = L.research_lib().lnx__crc32_variant
     f.restype = ctypes.c_int
@@ -23,94 +37,100 @@ def _lib():
     return f
 
 
-def _run(cuda, data, off, var=300):
+def _run(cuda, data, off, mode, verify=False):
+    """Results of the product entry (mode "auto" / "short") or research variant (int)."""
     import torch
+    import lneto_amd as L
     n = len(off) - 1
-    d = torch.from_numpy(data).to(cuda)
-    o = torch.from_numpy(off.astype(np.int64)).to(cuda)
-    out = torch.full((max(n, 1),), -1, dtype=torch.int32, device=cuda)
-    rc = _lib()(var, d.data_ptr(), o.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
-    torch.cuda.synchronize()
-    got = out.cpu().numpy().view(np.uint32)[:n]
-    return got if var % 2 == 0 else got.view(np.uint8)[:n]
+    d = data if isinstance(data, torch.Tensor) else torch.from_numpy(data).to(cuda)
+    o = torch.from_numpy(np.asarray(off).astype(np.int64)).to(cuda)
+    if isinstance(mode, int):
+        out = torch.full((max(n, 1),), -1, dtype=torch.int32, device=cuda)
+        rc = _research()(mode + int(verify), d.data_ptr(), o.data_ptr(), n, out.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)[:n]
+        return got.view(np.uint8)[:n] if verify else got
+    if verify:
+        return L.fcs_verify_batch(d, o, short_frames=mode == "short").cpu().numpy()
+    return L.crc32_batch(d, o, short_frames=mode == "short").cpu().numpy().view(np.uint32)
 
 
-def _check(cuda, off, seed, name, var=300):
+def _check(cuda, off, seed, name, mode):
     from lneto_amd import synth
     from oracle import oracle as O
     off = np.asarray(off, dtype=np.uint64)
-    data = synth.bytes_np(int(off[-1]) + 8, seed=seed)
-    got = _run(cuda, data, off, var)
+    data = synth.bytes_np(int(off.max()) + 8, seed=seed)
+    got = _run(cuda, data, off, mode)
     want = O.crc32_frames(data, off, threads=8)
     bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, f"{name}: wrong at frames {bad[:8]} (lens {np.diff(off)[bad[:8]]}) of {len(off) - 1}"
+    assert bad.size == 0, f"{name}: wrong at frames {bad[:8]} (lens {np.diff(off.astype(np.int64))[bad[:8]]}) of {len(off) - 1}"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", CRC_VARS)
-def test_gpu_stage_zipf(cuda, var):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_zipf(cuda, mode):
     from lneto_amd import synth
     for n, seed in ((1 << 16, 11), (1 << 20, 12), (300_001, 13)):
-        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}", var)
+        _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(n, seed=seed)), seed, f"zipf {n}", mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", CRC_VARS)
-def test_gpu_stage_all_lengths(cuda, var):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_all_lengths(cuda, mode):
     from lneto_amd import synth
     rng = np.random.default_rng(9)
     for lead in (0, 1, 2, 3, 5, 64, 127):
         lens = rng.permutation(np.arange(0, 701))
         off = np.concatenate([[0], synth.offsets_from_lengths(lens) + lead])
-        _check(cuda, off, 100 + lead, f"lengths lead {lead}", var)
+        _check(cuda, off, 100 + lead, f"lengths lead {lead}", mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", CRC_VARS)
-def test_gpu_stage_tiny_and_empty(cuda, var):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_tiny_and_empty(cuda, mode):
     """Several boundaries in one 64-byte half: the byte-serial path."""
     from lneto_amd import synth
     rng = np.random.default_rng(21)
     for trial in range(4):
         lens = rng.choice([0, 0, 1, 2, 3, 4, 5, 7, 9, 15, 16, 17, 33, 64, 200], size=20000 + 977 * trial)
         off = np.concatenate([[0], synth.offsets_from_lengths(lens) + trial * 37])
-        _check(cuda, off, 200 + trial, f"tiny {trial}", var)
+        _check(cuda, off, 200 + trial, f"tiny {trial}", mode)
     lens = np.concatenate([np.full(50000, 64), synth.zipf_lengths(50000, seed=5), np.full(3000, 1)])
-    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed", var)
+    _check(cuda, synth.offsets_from_lengths(lens), 300, "mixed", mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", CRC_VARS)
-def test_gpu_stage_long_frames(cuda, var):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_long_frames(cuda, mode):
     """Frames longer than a stretch (the carry runs through stretches without
     a boundary), jumbo frames, a 3 MiB frame among short ones."""
     from lneto_amd import synth
     rng = np.random.default_rng(31)
     lens = rng.choice([9000, 1500, 64, 0, 100_000], size=3000)
-    _check(cuda, synth.offsets_from_lengths(lens), 400, "long", var)
+    _check(cuda, synth.offsets_from_lengths(lens), 400, "long", mode)
     lens = np.array([60] * 500 + [3 << 20] + [60] * 500 + [1500] * 2000)
-    _check(cuda, synth.offsets_from_lengths(lens), 401, "3 MiB", var)
-    _check(cuda, synth.offsets_from_lengths(np.full(20000, 9000)), 402, "jumbo", var)
-    _check(cuda, synth.offsets_from_lengths(np.full(100000, 1500)), 403, "mtu", var)
+    _check(cuda, synth.offsets_from_lengths(lens), 401, "3 MiB", mode)
+    _check(cuda, synth.offsets_from_lengths(np.full(20000, 9000)), 402, "jumbo", mode)
+    _check(cuda, synth.offsets_from_lengths(np.full(100000, 1500)), 403, "mtu", mode)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("var", CRC_VARS)
-def test_gpu_stage_small_batches(cuda, var):
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_small_batches(cuda, mode):
     from lneto_amd import synth
     rng = np.random.default_rng(41)
     for n in (1, 2, 3, 63, 64, 65, 381, 382, 383, 765, 1000):
         lens = rng.integers(0, 400, size=n)
         for lead in (0, 13, 127):
-            _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(lens) + lead]), n + lead, f"n {n} lead {lead}", var)
+            _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(lens) + lead]), n + lead, f"n {n} lead {lead}",
+                   mode)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("var", [301, 303, 309, 311, 313, 315, 317, 319, 321, 323, 325, 327])
-def test_gpu_stage_verify(cuda, var):
-    """Variant 301: FCS verify (residue) over frames carrying their LE FCS;
-    a third get one flipped byte; runts under 4 bytes fail."""
+def _verify_case():
+    """200 000 Zipf frames carrying their LE FCS; a third get one flipped
+    byte; runts under 4 bytes fail."""
     from lneto_amd import synth
     from oracle import oracle as O
     lens = synth.zipf_lengths(200_000, seed=7)
@@ -127,39 +147,178 @@ def test_gpu_stage_verify(cuda, var):
         s, e = int(off[i]), int(off[i + 1])
         if e > s:
             data[s + int(rng.integers(0, e - s))] ^= 0x40
-    got = _run(cuda, data, off, var=var)
     want = np.array([int(int(off[i + 1]) - int(off[i]) >= 4 and O.c_crc32(data[int(off[i]):int(off[i + 1])].tobytes())
                          == 0x2144DF1C) for i in range(len(lens))], dtype=np.uint8)
-    bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, bad[:10]
     assert want.sum() > 100_000 and (want == 0).sum() > 50_000
+    return data, off, want
 
 
 @pytest.mark.gpu
-def test_gpu_short_frames_entry(cuda):
-    """The product entry (lnx_crc32_batch_ex / lnx_fcs_verify_batch_ex with
-    LNX_BATCH_SHORT_FRAMES, and lnx_crc32_batch_host, which picks the staged
-    kernel itself for a short mix) against the oracle."""
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_stage_verify(cuda, mode):
+    data, off, want = _verify_case()
+    got = _run(cuda, data, off, mode, verify=True)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_offsets_out_of_order(cuda, mode):
+    """Offsets outside the contract (an end below its start): such a frame is
+    empty, the others are CRC32(bytes[off[i]:off[i+1]]) whichever kernel folds
+    them (off = [0, 8, 4, 12]); in a long staged slice the block
+    with the reversed pair is folded one lane per frame (ooo_block)."""
+    from lneto_amd import synth
+    _check(cuda, np.array([0, 8, 4, 12]), 70, "0 8 4 12", mode)
+    off = synth.offsets_from_lengths(synth.zipf_lengths(100_000, seed=71)).astype(np.int64)
+    for i in (5, 777, 40_001, 99_990):
+        off[i] = off[i + 1] + 3  # frame i - 1 runs long, frame i is empty (end below start)
+    _check(cuda, off.astype(np.uint64), 72, "zipf with reversed pairs", mode)
+
+
+@pytest.mark.gpu
+def test_gpu_dispatch_mixed_slices(cuda):
+    """One batch whose slices go to different kernels under the default entry
+    (uniform 1500 B, 256 B and 9000 B slices to the rows kernel; Zipf, 64 B and
+    uniform-random slices to the staged one), every frame against the oracle."""
+    from lneto_amd import synth
+    rng = np.random.default_rng(81)
+    parts = [np.full(300_000, 1500), synth.zipf_lengths(400_000, seed=82), np.full(200_000, 256),
+             np.full(300_000, 64), np.full(20_000, 9000), rng.integers(64, 1500, 150_000), np.full(70_000, 1024)]
+    lens = np.concatenate(parts)
+    _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(lens) + 3]), 83, "mixed slices", "auto")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_configs3_full_batch(cuda, mode):
+    """configs[3] whole: 16 M Zipf frames, 4.13 GB, offsets past 2^31 and
+    2^32, frame by frame against the C oracle (16 threads, Go's amd64 path)."""
     import torch
+    from lneto_amd import synth
+    from oracle import oracle as O
+    off = synth.offsets_from_lengths(synth.zipf_lengths(1 << 24))
+    assert int(off[-1]) > (1 << 32)
+    d = synth.bytes_torch(int(off[-1]), cuda)
+    got = _run(cuda, d, off, mode)
+    want = O.crc32_frames(d.cpu().numpy(), off, threads=16, amd64=O.has_clmul())
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:10]
+    del d
+    torch.cuda.empty_cache()
+
+
+def _giant_batch(lead, giant, nshort, at, seed=91):
+    """nshort short Zipf frames with one frame of `giant` bytes at index `at`."""
+    from lneto_amd import synth
+    lens = synth.zipf_lengths(nshort, seed=seed).astype(np.int64)
+    lens = np.insert(lens, at, giant)
+    return np.concatenate([[0], synth.offsets_from_lengths(lens) + lead]).astype(np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_giant_frame(cuda, mode):
+    """a 2.2 GB frame among 2000 short ones with a nonzero
+    lead-in.  Its slice does not fit 31-bit offsets: every workgroup of the
+    staged launch folds 16 KiB pieces of it and joins the parts (giant_pieces).
+    CRC and FCS verify against the C oracle, and the launch time."""
+    import torch
+    from lneto_amd import synth
+    from oracle import oracle as O
+    import lneto_amd as L
+    giant = 2_200_000_000
+    off = _giant_batch(5, giant, 2000, 1234)
+    d = synth.bytes_torch(int(off[-1]) + 8, cuda, seed=92)
+    host = d.cpu().numpy()
+    want = O.crc32_frames(host, off, threads=16, amd64=O.has_clmul())
+    got = _run(cuda, d, off, mode)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, bad[:10]
+    # the giant frame carries its FCS: it verifies, a flipped byte in its middle fails it
+    s, e = int(off[1234]), int(off[1235])
+    d[e - 4:e] = torch.tensor(list(int(O.crc32_frames(host, np.array([s, e - 4], np.uint64), amd64=O.has_clmul())[0])
+                                   .to_bytes(4, "little")), dtype=torch.uint8, device=cuda)
+    ok = _run(cuda, d, off, mode, verify=True)
+    assert ok[1234] == 1 and (ok[:1234] == ((want[:1234] == 0x2144DF1C) & (np.diff(off.astype(np.int64))[:1234] >= 4))).all()
+    d[s + giant // 2 + 7] ^= 1
+    ok = _run(cuda, d, off, mode, verify=True)
+    assert ok[1234] == 0
+    # the launch: HIP events around the entry on the current stream
+    o = torch.from_numpy(off.astype(np.int64)).to(cuda)
+    c = torch.empty(len(off) - 1, dtype=torch.int32, device=cuda)
+    ts = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        L.crc32_batch(d, o, out=c, short_frames=mode == "short")
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ms = float(np.median(ts))
+    print(f"giant frame {giant} B among 2000: {ms:.3f} ms ({int(off[-1]) / ms / 1e6:.0f} GB/s)")
+    assert ms < 50.0, ts
+    del d, host
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_giant_slices_edges(cuda):
+    """Giant slices with frames ending exactly on 16 KiB piece bounds, empty
+    frames at a giant slice's start and end, two giant frames in one slice and
+    a giant slice beside ordinary ones (3 000 frames: 47 slices)."""
+    import torch
+    from lneto_amd import synth
+    from oracle import oracle as O
+    P = 16384
+    rng = np.random.default_rng(93)
+    lens = list(rng.integers(0, 3000, 1350))  # (the group below: frames 1350-1362, all in slice 21 = [1344, 1408))
+    lens += [0, 0, P - 100, P, 3 * P, 1, 1_150_000_000, 0, 7, 1_100_000_000 + 13, 2 * P, 0, 0]
+    lens += list(rng.integers(0, 3000, 1637))
+    off = np.concatenate([[0], synth.offsets_from_lengths(np.array(lens)) + 100]).astype(np.uint64)
+    d = synth.bytes_torch(int(off[-1]) + 8, cuda, seed=94)
+    want = O.crc32_frames(d.cpu().numpy(), off, threads=16, amd64=O.has_clmul())
+    for mode in MODES:
+        got = _run(cuda, d, off, mode)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (mode, bad[:10])
+    del d
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_short_frames_entry_host(cuda):
+    """lnx_crc32_batch_host (the plain entry's dispatch behind pinned copies)
+    against the oracle."""
     import lneto_amd as L
     from lneto_amd import synth
     from oracle import oracle as O
     rng = np.random.default_rng(51)
     cases = [synth.offsets_from_lengths(synth.zipf_lengths(300_001, seed=3)),
              np.concatenate([[0], synth.offsets_from_lengths(rng.permutation(np.arange(0, 701))) + 5]),
-             np.concatenate([[0], synth.offsets_from_lengths(rng.choice([0, 1, 3, 17, 64, 65], size=30000)) + 1])]
+             np.array([0, 8, 4, 12])]
     for k, off in enumerate(cases):
-        off = np.asarray(off, dtype=np.int64)
-        data = synth.bytes_np(int(off[-1]) + 8, seed=60 + k)
-        want = O.crc32_frames(data, off.astype(np.uint64), threads=8)
-        d = torch.from_numpy(data).to(cuda)
-        o = torch.from_numpy(off).to(cuda)
-        got = L.crc32_batch(d, o, short_frames=True).cpu().numpy().view(np.uint32)
-        assert (got == want).all(), (k, np.nonzero(got != want)[0][:8])
-        ok = L.fcs_verify_batch(d, o, short_frames=True).cpu().numpy()
-        lens = np.diff(off)
-        assert (ok == ((want == 0x2144DF1C) & (lens >= 4))).all(), k
+        off = np.asarray(off, dtype=np.uint64)
+        data = synth.bytes_np(int(off.max()) + 8, seed=60 + k)
+        want = O.crc32_frames(data, off, threads=8)
         host = np.zeros(len(off) - 1, dtype=np.uint32)
-        assert L.lib.lnx_crc32_batch_host(data.ctypes.data, data.size, off.astype(np.uint64).ctypes.data,
-                                          len(off) - 1, host.ctypes.data, 0) == 0
+        assert L.lib.lnx_crc32_batch_host(data.ctypes.data, data.size, off.ctypes.data, len(off) - 1,
+                                          host.ctypes.data, 0) == 0
         assert (host == want).all(), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var", RESEARCH_VARS)
+def test_gpu_research_stage_form(cuda, var):
+    """One parity test per round-4 research form: the Zipf mix, all lengths at
+    a lead-in, tiny frames, and its FCS verify form."""
+    from lneto_amd import synth
+    _check(cuda, synth.offsets_from_lengths(synth.zipf_lengths(1 << 16, seed=11)), 11, "zipf", var)
+    rng = np.random.default_rng(9)
+    _check(cuda, np.concatenate([[0], synth.offsets_from_lengths(rng.permutation(np.arange(0, 701))) + 5]), 105,
+           "lengths", var)
+    _check(cuda, synth.offsets_from_lengths(rng.choice([0, 1, 3, 17, 64, 65, 3000], size=20000)), 106, "tiny", var)
+    data, off, want = _verify_case()
+    got = _run(cuda, data, off, var, verify=True)
+    assert (got == want).all(), np.nonzero(got != want)[0][:10]

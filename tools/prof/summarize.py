@@ -51,6 +51,7 @@ def main():
                     js = json.loads(line)
                     steps = int(js.get("steps", steps))
                     summary["lnx_version"] = js.get("config", {}).get("kernel")
+                    summary["build_id"] = js.get("config", {}).get("build_id")
         except (OSError, ValueError):
             pass
         if d:
@@ -86,7 +87,7 @@ def main():
     keys = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT")
     if all(k in c for k in keys):  # read by bench.py (roofline_compute): tied to the build that made them
         with open(os.path.join(dst, f"counters_{wl}.json"), "w") as fh:
-            json.dump({**{k: c[k] for k in keys}, "lnx_version": summary.get("lnx_version"),
+            json.dump({**{k: c[k] for k in keys}, "build_id": summary.get("build_id"),
                        "clock_ghz_est": summary.get("clock_ghz_est"), "source": f"{tag}_{wl}_summary.json",
                        "method": "rocprofv3 --pmc, one counter group per pass (tools/prof/profile.sh), per-launch "
                                  "averages over the traced dispatches; SQ_* summed over all CUs"}, fh, indent=1)
