@@ -76,6 +76,33 @@ uint16_t lnx_sum16_payload(uint32_t sum, const uint8_t* p, size_t n);
 /* Go: lneto.NeverZeroSum (crc.go:65-71). */
 uint16_t lnx_never_zero_sum(uint16_t sum16);
 
+/* The receive path's checksum-stage verdict of ONE Ethernet frame (FCS
+ * stripped) on the host: the value lnx_ingress_verify_batch_filtered computes
+ * per frame (StackEthernet.Demux, internet/stack-ethernet.go:139-165, then
+ * demux4 / demux6, internet/stack-ip4.go:100-164, internet/stack-ip6.go:86-138;
+ * codes and flags as documented there; filter NULL = accept-all).  Returns the
+ * verdict (>= 0) or LNX_EINVAL.  The packet entries (lnx_ingress_packets,
+ * lnx_rx_ring_ingress) use it for batches below their host threshold, so
+ * netdev's one-buffer-per-call Runner (x/netdev/runner.go:432-433) never
+ * launches a kernel. */
+#define LNX_VERIFY_EVIL_BIT 1u /* lneto.ValidateEvilBit on the stack's Validator */
+#define LNX_VERIFY_ICMP 2u     /* the ICMPv4 / ICMPv6 clients are attached (StackAsync.EnableICMP) */
+struct lnx_rx_filter;
+int lnx_ingress_verdict(const uint8_t* frame, size_t len, uint32_t flags, const struct lnx_rx_filter* filter);
+
+/* The transmit checksum step of ONE frame on the host, in place: the per-frame
+ * semantics of lnx_tx_checksum_batch (encapsulate4 / encapsulate6 / the ICMP
+ * clients, internet/stack-ip4.go:202-228, internet/stack-ip6.go:167-181).
+ * Returns the status (0, 18 ErrTruncatedFrame, 15 ErrInvalidLengthField) or
+ * LNX_EINVAL. */
+int lnx_tx_checksum(uint8_t* frame, size_t len);
+
+/* StackEthernet.Encapsulate's tail with the CRC32Update hook set, ONE frame on
+ * the host (internet/stack-ethernet.go:200-214): zero-pad to 60 bytes, append
+ * the LE FCS, *len = the new length; 6 (ErrShortBuffer) with the frame
+ * untouched when it would outgrow `capacity`; LNX_EINVAL for NULL pointers. */
+int lnx_fcs_append(uint8_t* frame, uint32_t* len, uint32_t capacity);
+
 /* ======================================================================== *
  * 2. Batched device-resident HIP path (gfx950)
  * ======================================================================== */
@@ -185,8 +212,6 @@ int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const 
  * configuration and are taken as accept-all.  With LNX_VERIFY_ICMP, ICMP
  * messages also take their client's Demux checks up to the checksum
  * (ipv4/icmpv4/client.go:89-102, ipv6/icmpv6/client.go:100-115). */
-#define LNX_VERIFY_EVIL_BIT 1u /* lneto.ValidateEvilBit on the stack's Validator */
-#define LNX_VERIFY_ICMP 2u     /* the ICMPv4 / ICMPv6 clients are attached (StackAsync.EnableICMP) */
 int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                              uint8_t* d_verdict, void* stream);
 
@@ -209,7 +234,7 @@ int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint
  *     it is ff00::/8 (internal/ip.go:30-38); a next header with no handler is
  *     dropped before the sums.
  * A NULL filter is accept-all (lnx_ingress_verify_batch). */
-typedef struct lnx_rx_filter {
+typedef struct lnx_rx_filter {  /* (EtherTypes must be > 1500: RegisterEthernet, stack-ethernet.go:131-135) */
   uint8_t mac[6];                 /* StackEthernetConfig.MAC */
   uint8_t eth_accept_multicast;   /* StackEthernet.SetAcceptMulticast */
   uint8_t ip4_accept_multicast;   /* stackip4 SetAcceptMulticast / SetAcceptBroadcast */
@@ -264,6 +289,26 @@ uint32_t* lnx_rx_ring_lengths(lnx_rx_ring* ring);
 /* The ring's stack configuration for its verdicts (a copy of *filter is
  * kept; NULL = accept-all, the default).  LNX_EINVAL for more than 8 EtherTypes. */
 int lnx_rx_ring_set_filter(lnx_rx_ring* ring, const lnx_rx_filter* filter);
+
+/* Batches of fewer than `frames` frames (lnx_rx_ring_ingress counts,
+ * lnx_ingress_packets / lnx_egress_packets n) run on the host with the
+ * per-frame functions above (lnx_ingress_verdict, lnx_tx_checksum,
+ * lnx_fcs_append, the residue test): no kernel launch, no copy.  The default,
+ * LNX_HOST_BATCH_DEFAULT, is the measured crossover of the GPU round trip
+ * (DESIGN.md §4 "per-call latency"); 0 sends every batch to the GPU. */
+#define LNX_HOST_BATCH_DEFAULT 64u
+int lnx_rx_ring_set_host_threshold(lnx_rx_ring* ring, uint32_t frames);
+
+/* Where the ring's frames went since it was created (in the spirit of netdev's
+ * RunnerStatistics, x/netdev/runner.go:107-140): frames folded on the host
+ * below the threshold, frames and batches (one H2D / kernels / D2H round
+ * trip each) sent to the GPU. */
+typedef struct lnx_rx_ring_counters {
+  uint64_t host_frames;
+  uint64_t device_frames;
+  uint64_t device_batches;
+} lnx_rx_ring_counters;
+int lnx_rx_ring_stats(lnx_rx_ring* ring, lnx_rx_ring_counters* out);
 
 /* Device delivers frames without their FCS (x/netdev/interface.go:34-40 leaves
  * the FCS to "device or stack"): no FCS check (fcs_ok = 1), verdicts on the

@@ -22,6 +22,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -207,9 +208,12 @@ struct StackFilter {
   std::vector<uint16_t> EtherTypes{0x0800, 0x86DD, 0x0806};
   std::vector<uint8_t> Protocols4{1, 6, 17}, Protocols6{6, 17, 58};
 
-  // The C-ABI form; false for more than 8 EtherTypes.
+  // The C-ABI form; false for more than 8 EtherTypes or one RegisterEthernet
+  // rejects (proto <= 1500 -> ErrInvalidConfig, internet/stack-ethernet.go:131-135).
   bool ToC(lnx_rx_filter* f) const {
     if (EtherTypes.size() > 8) return false;
+    for (uint16_t et : EtherTypes)
+      if (et <= 1500) return false;
     *f = lnx_rx_filter{};
     for (int i = 0; i < 6; ++i) f->mac[i] = MAC[i];
     f->eth_accept_multicast = AcceptMulticastEthernet, f->ip4_accept_multicast = AcceptMulticast4;
@@ -311,6 +315,13 @@ class RxRing {
   }
   uint32_t Slots() const { return nslots_; }
   uint32_t SlotCap() const { return cap_; }
+  // Batches below `frames` run on the host (no launch); 0 = always the GPU.
+  int SetHostThreshold(uint32_t frames) { return lnx_rx_ring_set_host_threshold(r_, frames); }
+  lnx_rx_ring_counters Stats() const {
+    lnx_rx_ring_counters c{};
+    (void)lnx_rx_ring_stats(r_, &c);
+    return c;
+  }
 
  private:
   uint32_t flags(bool evilBit) const { return (evilBit ? LNX_VERIFY_EVIL_BIT : 0u) | (noFCS_ ? LNX_RX_NO_FCS : 0u); }
@@ -319,5 +330,50 @@ class RxRing {
   bool noFCS_ = false;
   std::vector<const uint8_t*> ptrs_;
   std::vector<uint32_t> lens_;
+};
+
+// The batching half of a netdev Runner (x/netdev/runner.go:420-476) for the
+// ring: the reference's Runner hands IngressPackets ONE buffer per call
+// (r.bufsaux = [1][]byte{buf}, :432-433,469-470) and releases it at once.
+// RxBatcher keeps the receive handler's shape — Put copies an incoming frame
+// into the next free pinned slot, as bufferSelect.goroPutRx copies it into a
+// free buffer (x/netdev/buffer.go:77-98) — but Drain hands every pending slot
+// to ONE Ingress call (up to Slots() frames), then frees them all; Put drains
+// by itself when the slots are full.  The callback gets each frame's index in
+// Put order, its FCS verdict and its receive verdict.  INTEGRATION.md §2.2
+// has the same loop in Go.
+class RxBatcher {
+ public:
+  using OnFrame = void (*)(void* ctx, uint64_t index, uint8_t fcsOK, uint8_t verdict);
+  RxBatcher(RxRing& ring, OnFrame on, void* ctx) : ring_(ring), on_(on), ctx_(ctx) {}
+  // false: frame longer than a slot (dropped, as goroPutRx drops it)
+  bool Put(const uint8_t* frame, uint32_t len) {
+    if (len > ring_.SlotCap()) return false;
+    if (pending_ == ring_.Slots() && Drain() != LNX_OK) return false;
+    std::memcpy(ring_.Slot(pending_), frame, len);
+    ring_.Len(pending_) = len;
+    ++pending_;
+    return true;
+  }
+  int Drain() {
+    if (pending_ == 0) return LNX_OK;
+    ok_.resize(pending_);
+    verdict_.resize(pending_);
+    const int rc = ring_.Ingress(0, pending_, 0, ok_.data(), verdict_.data());
+    if (rc == LNX_OK)
+      for (uint32_t k = 0; k < pending_; ++k) on_(ctx_, next_ + k, ok_[k], verdict_[k]);
+    next_ += pending_;
+    pending_ = 0;
+    return rc;
+  }
+  uint32_t Pending() const { return pending_; }
+
+ private:
+  RxRing& ring_;
+  OnFrame on_;
+  void* ctx_;
+  uint32_t pending_ = 0;
+  uint64_t next_ = 0;
+  std::vector<uint8_t> ok_, verdict_;
 };
 }  // namespace netdev

@@ -79,6 +79,9 @@ class RxFilter(ctypes.Structure):
              ip6_accept_multicast: bool = False) -> "RxFilter":
         if len(mac) != 6 or len(ip4) != 4 or len(ip6) != 16 or len(ethertypes) > 8:
             raise LnetoError("RxFilter: mac 6 bytes, ip4 4, ip6 16, at most 8 EtherTypes")
+        if any(et <= 1500 or et > 0xFFFF for et in ethertypes):
+            # RegisterEthernet: proto > MaxUint16 || proto <= 1500 -> ErrInvalidConfig (internet/stack-ethernet.go:131-135)
+            raise LnetoError("RxFilter: EtherTypes must be in (1500, 0xFFFF] (RegisterEthernet)")
         f = cls()
         f.mac[:] = list(mac)
         f.ip4[:] = list(ip4)
@@ -411,6 +414,7 @@ VERIFY_EVIL_BIT = 1  # LNX_VERIFY_EVIL_BIT
 VERIFY_ICMP = 2      # LNX_VERIFY_ICMP
 RX_NO_FCS = 4        # LNX_RX_NO_FCS: the device strips the FCS (x/netdev/interface.go:34-40)
 TX_CHECKSUM, TX_FCS = 1, 2  # LNX_TX_CHECKSUM, LNX_TX_FCS
+HOST_BATCH_DEFAULT = 64  # LNX_HOST_BATCH_DEFAULT: packet batches below it run on the host
 
 
 def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None, filter: RxFilter | None = None):
@@ -506,18 +510,32 @@ class RxRing:
     takes caller-owned buffers instead (IngressPackets(bufs, offset) exactly).
     """
 
-    def __init__(self, nslots: int, slot_cap: int = 2048, batch_slots: int = 0, depth: int = 3, device: int = 0):
+    def __init__(self, nslots: int, slot_cap: int = 2048, batch_slots: int = 0, depth: int = 3, device: int = 0,
+                 host_threshold: int | None = None):
         import numpy as np
         h = _vp()
         _check(lib.lnx_rx_ring_create(device, nslots, slot_cap, batch_slots, depth, ctypes.byref(h)),
                "lnx_rx_ring_create")
         self._h = h
+        if host_threshold is not None:
+            self.set_host_threshold(host_threshold)
         self.nslots, self.slot_cap = nslots, slot_cap
         sp = lib.lnx_rx_ring_slots(h)
         lp = lib.lnx_rx_ring_lengths(h)
         self.slots = np.ctypeslib.as_array((ctypes.c_uint8 * (nslots * slot_cap)).from_address(sp)).reshape(
             nslots, slot_cap)
         self.lengths = np.ctypeslib.as_array((ctypes.c_uint32 * nslots).from_address(lp))
+
+    def set_host_threshold(self, frames: int) -> None:
+        """Batches of fewer frames run on the host, no launch (lnx_rx_ring_set_host_threshold;
+        HOST_BATCH_DEFAULT unless set; 0 = every batch on the GPU)."""
+        _check(lib.lnx_rx_ring_set_host_threshold(self._h, frames), "lnx_rx_ring_set_host_threshold")
+
+    def stats(self) -> dict:
+        """{host_frames, device_frames, device_batches} since creation (lnx_rx_ring_stats)."""
+        c = (ctypes.c_uint64 * 3)()
+        _check(lib.lnx_rx_ring_stats(self._h, c), "lnx_rx_ring_stats")
+        return {"host_frames": c[0], "device_frames": c[1], "device_batches": c[2]}
 
     def set_filter(self, filt: RxFilter | None) -> None:
         """The ring's stack configuration (lnx_rx_ring_set_filter); None = accept-all."""

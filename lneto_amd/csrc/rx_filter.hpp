@@ -23,11 +23,16 @@ struct RxFilter {
 
 inline uint32_t le32_of(const uint8_t* b) { return b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24); }
 
-// NULL: accept-all.  Returns false for a filter with more than 8 EtherTypes.
+// NULL: accept-all.  Returns false for a filter with more than 8 EtherTypes,
+// or with an EtherType the stack cannot register: RegisterEthernet rejects
+// proto <= 1500 (802.3 length values) with ErrInvalidConfig
+// (internet/stack-ethernet.go:131-135), so such a frame always ends in DROP.
 inline bool rx_filter_of(const lnx_rx_filter* f, RxFilter* out) {
   RxFilter r{};
   if (f) {
     if (f->n_ethertypes > 8) return false;
+    for (uint32_t i = 0; i < f->n_ethertypes; ++i)
+      if (f->ethertypes[i] <= 1500) return false;
     r.on = 1;
     r.mac_lo = le32_of(f->mac);
     r.mac_hi = f->mac[4] | (f->mac[5] << 8);

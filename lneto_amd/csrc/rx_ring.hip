@@ -50,6 +50,11 @@ int device_resources(const void** image, int* num_cus, const void** stage_image)
 int crc_offsets(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify, uint32_t policy,
                 hipStream_t stream);
 int hip_error(hipError_t e, const char* what);
+// host_path.cpp: the per-frame host forms (batches below the ring's host threshold)
+uint8_t host_verdict(const uint8_t* fr, size_t L, uint32_t flags, const RxFilter& f);
+uint8_t host_tx_checksum(uint8_t* f, size_t L);
+uint8_t host_fcs_append(uint8_t* f, uint32_t* len, uint32_t capacity);
+uint8_t host_fcs_ok(const uint8_t* f, size_t L);
 hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                                       uint8_t* ok, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
@@ -99,6 +104,10 @@ struct lnx_rx_ring {
   };
   std::vector<Stage> st;
   RxFilter filt{};  // lnx_rx_ring_set_filter; on = 0: accept-all
+  // batches of fewer frames run on the host (host_path.cpp), no launch
+  // (lnx_rx_ring_set_host_threshold; the default is the measured crossover)
+  uint32_t host_below = LNX_HOST_BATCH_DEFAULT;
+  lnx_rx_ring_counters stats{};  // lnx_rx_ring_stats (RunnerStatistics-style, x/netdev/runner.go:107-140)
   const void* image = nullptr;
   const void* stage_image = nullptr;  // the staged lane streams' tables (short-frame batches)
   int num_cus = 0;
@@ -213,6 +222,8 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
   if ((e = hipMemcpyAsync(ok_dst, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(verdict_dst, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
     return hip_error(e, "rx ring D2H");
+  r->stats.device_batches += 1;
+  r->stats.device_frames += nb;
   return LNX_OK;
 }
 
@@ -241,12 +252,37 @@ int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t c
       (e = hipMemcpyAsync(s.h_ok, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(s.h_verdict, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
     return hip_error(e, "tx ring D2H");
+  r->stats.device_batches += 1;
+  r->stats.device_frames += nb;
   return LNX_OK;
+}
+
+// The receive step of one frame on the host: frame = p[0 : len], FCS in its
+// last 4 bytes unless LNX_RX_NO_FCS (the semantics of enqueue_rx).
+void host_rx(const lnx_rx_ring* r, const uint8_t* p, uint32_t len, uint32_t flags, uint8_t* ok, uint8_t* verdict) {
+  const bool fcs = !(flags & LNX_RX_NO_FCS);
+  const uint32_t trim = fcs ? 4u : 0u;
+  *ok = fcs ? host_fcs_ok(p, len) : 1u;
+  *verdict = host_verdict(p, len > trim ? len - trim : 0u, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP), r->filt);
 }
 
 }  // namespace
 
 extern "C" {
+
+int lnx_rx_ring_stats(lnx_rx_ring* r, lnx_rx_ring_counters* out) {
+  if (!r || !out) return LNX_EINVAL;
+  std::lock_guard<std::mutex> lk(r->mu);
+  *out = r->stats;
+  return LNX_OK;
+}
+
+int lnx_rx_ring_set_host_threshold(lnx_rx_ring* r, uint32_t frames) {
+  if (!r) return LNX_EINVAL;
+  std::lock_guard<std::mutex> lk(r->mu);
+  r->host_below = frames;
+  return LNX_OK;
+}
 
 int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t batch_slots, uint32_t depth,
                        lnx_rx_ring** out) {
@@ -319,6 +355,17 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
   if ((uint64_t)first + count > r->nslots || offset >= r->cap) return LNX_EINVAL;
   if (count == 0) return LNX_OK;
   std::lock_guard<std::mutex> lk(r->mu);
+  if (count < r->host_below) {  // below the crossover: no launch
+    for (uint32_t i = first; i < first + count; ++i) {
+      const uint32_t l = std::min(r->h_len[i], r->cap);
+      uint8_t ok, v;
+      host_rx(r, r->h_slots + (size_t)i * r->cap + offset, l > offset ? l - offset : 0u, flags, &ok, &v);
+      if (fcs_ok) fcs_ok[i - first] = ok;
+      if (verdict) verdict[i - first] = v;
+    }
+    r->stats.host_frames += count;
+    return LNX_OK;
+  }
   hipError_t e = hipSetDevice(r->device);
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   int rc = LNX_OK;
@@ -364,6 +411,16 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
     if (lens[i] > r->cap || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   std::lock_guard<std::mutex> lk(r->mu);
+  if (n < r->host_below) {  // below the crossover: no launch (netdev's Runner hands over one buffer per call)
+    for (uint64_t i = 0; i < n; ++i) {
+      uint8_t ok, v;
+      host_rx(r, bufs[i] + offset, lens[i] > offset ? lens[i] - offset : 0u, flags, &ok, &v);
+      if (fcs_ok) fcs_ok[i] = ok;
+      if (verdict) verdict[i] = v;
+    }
+    r->stats.host_frames += n;
+    return LNX_OK;
+  }
   hipError_t e = hipSetDevice(r->device);
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   // Batches go round-robin over the stages; batch k is packed into the
@@ -412,6 +469,18 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     if (lens[i] > capacity || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   std::lock_guard<std::mutex> lk(r->mu);
+  if (n < r->host_below) {  // below the crossover: no launch
+    for (uint64_t i = 0; i < n; ++i) {
+      uint8_t* f = bufs[i] + offset;
+      uint32_t l = lens[i];
+      const uint8_t ck = (flags & LNX_TX_CHECKSUM) ? host_tx_checksum(f, l) : 0u;
+      const uint8_t ap = (flags & LNX_TX_FCS) ? host_fcs_append(f, &l, capacity) : 0u;
+      lens[i] = l;
+      if (status) status[i] = ck ? ck : ap;
+    }
+    r->stats.host_frames += n;
+    return LNX_OK;
+  }
   hipError_t e = hipSetDevice(r->device);
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   // as lnx_ingress_packets: batches round-robin over the stages, the gather of

@@ -156,6 +156,70 @@ static void TestRxRingFilter(netdev::RxRing& ring) {
   ring.SetDeviceStripsFCS(false);
 }
 
+// netdev's Runner calls IngressPackets with ONE buffer per call
+// (x/netdev/runner.go:432-433,469-470): through the ring that pattern must
+// never launch a kernel (the host path below the threshold), and the batching
+// loop (netdev::RxBatcher: Put per received frame, one Ingress per drain)
+// must reach the GPU in whole batches — with identical results either way,
+// equal to the per-frame host functions.
+struct Collected {
+  std::vector<uint8_t> ok, verdict;
+};
+static void collect(void* ctx, uint64_t i, uint8_t ok, uint8_t v) {
+  auto* c = static_cast<Collected*>(ctx);
+  if (c->ok.size() <= i) c->ok.resize(i + 1), c->verdict.resize(i + 1);
+  c->ok[i] = ok, c->verdict[i] = v;
+}
+static void TestRunnerPatterns() {
+  netdev::RxRing ring;
+  EXPECT(ring.Open(0, 1024, 256, 512, 2) == LNX_OK, "ring open");
+  const uint8_t us[6] = {0xc0, 0xff, 0xee, 0, 0xde, 0xad}, ip_us[4] = {192, 168, 10, 2};
+  internet::StackEthernetConfig cfg;
+  cfg.CRC32Update = ethernet::CRC32Update;
+  const int kFrames = 3000;
+  std::vector<std::vector<uint8_t>> frames(kFrames);
+  for (int k = 0; k < kFrames; ++k) {
+    std::vector<uint8_t> f = udpFrame(us, ip_us);
+    f.resize(f.size() + 68, 0);
+    size_t n = internet::AppendFCS(f.data(), 52, cfg);
+    f.resize(n);
+    if (k % 7 == 3) f[20 + k % 30] ^= 0x04;   // some bad sums / bad FCS
+    if (k % 11 == 5) f[n - 1] ^= 0x80;        // a bad FCS only
+    frames[k] = f;
+  }
+  // the reference's pattern: one buffer per call
+  const lnx_rx_ring_counters c0 = ring.Stats();
+  std::vector<uint8_t> ok1(kFrames), v1(kFrames);
+  for (int k = 0; k < kFrames; ++k) {
+    std::vector<lneto::Bytes> one = {lneto::Bytes(frames[k].data(), frames[k].size())};
+    std::vector<uint8_t> ok, v;
+    EXPECT(ring.IngressPackets(one, 0, ok, v) == LNX_OK, "one-frame ingress %d", k);
+    ok1[k] = ok[0], v1[k] = v[0];
+  }
+  const lnx_rx_ring_counters c1 = ring.Stats();
+  EXPECT(c1.device_batches == c0.device_batches, "one frame per call launched %llu batches",
+         (unsigned long long)(c1.device_batches - c0.device_batches));
+  EXPECT(c1.host_frames - c0.host_frames == uint64_t(kFrames), "host frames %llu",
+         (unsigned long long)(c1.host_frames - c0.host_frames));
+  // the batching loop: every frame Put into a slot, one Ingress per 1024 frames
+  Collected got;
+  netdev::RxBatcher batcher(ring, collect, &got);
+  for (int k = 0; k < kFrames; ++k) EXPECT(batcher.Put(frames[k].data(), uint32_t(frames[k].size())), "put %d", k);
+  EXPECT(batcher.Drain() == LNX_OK, "drain");
+  const lnx_rx_ring_counters c2 = ring.Stats();
+  EXPECT(c2.device_batches - c1.device_batches == 6, "batched: %llu device batches (1024 + 1024 + 952 frames, 512 "
+         "per stage)", (unsigned long long)(c2.device_batches - c1.device_batches));
+  EXPECT(c2.device_frames - c1.device_frames == uint64_t(kFrames), "device frames");
+  int bad = 0;
+  for (int k = 0; k < kFrames; ++k) {
+    const auto& f = frames[k];
+    const uint8_t wok = ethernet::CRC32(lneto::Bytes(f.data(), f.size())) == LNX_CRC32_RESIDUE;
+    const int wv = lnx_ingress_verdict(f.data(), f.size() - 4, 0, nullptr);
+    bad += ok1[k] != wok || v1[k] != wv || got.ok[k] != wok || got.verdict[k] != wv;
+  }
+  EXPECT(bad == 0, "%d frames differ between the host path, the batched GPU path and the per-frame functions", bad);
+}
+
 // The receive ring through the C++ mirror: without a GPU it must refuse to
 // open (no silent CPU path); with one, a valid and a corrupted frame.
 static void TestRxRing() {
@@ -197,6 +261,7 @@ static void TestRxRing() {
   EXPECT(c.PayloadSum16(lneto::Bytes(e + 34, 18)) == 0, "egress UDP CRC verifies");
   EXPECT(buf[0] == 0xEE && buf[1] == 0xEE && buf[2 + 64] == 0xEE, "bytes outside the frame untouched");
   TestRxRingFilter(ring);
+  TestRunnerPatterns();
 }
 
 int main() {

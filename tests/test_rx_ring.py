@@ -41,6 +41,12 @@ def _expect(frames):
     return ok, verdict
 
 
+def _ring(*a, **kw):
+    """A ring whose batches all go to the GPU (host threshold 0), whatever their size."""
+    kw.setdefault("host_threshold", 0)
+    return L.RxRing(*a, **kw)
+
+
 def _cap_for(frames, offset):
     """Slot capacity: the largest buffer, rounded up to 4 bytes."""
     return (max(len(f) for f in frames) + offset + 3) & ~3
@@ -59,7 +65,7 @@ def test_ring_requires_a_device():
 def test_ring_slots_ingress(cuda, offset):
     frames = _case_frames(seed=11 + offset, count=1200)
     cap = _cap_for(frames, offset)
-    ring = L.RxRing(len(frames) + 7, slot_cap=cap, batch_slots=256, depth=3)
+    ring = _ring(len(frames) + 7, slot_cap=cap, batch_slots=256, depth=3)
     try:
         for i, f in enumerate(frames):
             ring.slots[i + 7, :offset] = 0xEE  # headroom before the frame
@@ -78,7 +84,7 @@ def test_ring_slots_ingress(cuda, offset):
 @pytest.mark.gpu
 def test_ring_evil_bit_flag(cuda):
     frames = _case_frames(seed=5, count=600)
-    ring = L.RxRing(len(frames), slot_cap=_cap_for(frames, 0), batch_slots=200, depth=2)
+    ring = _ring(len(frames), slot_cap=_cap_for(frames, 0), batch_slots=200, depth=2)
     try:
         ok, verdict = ring.ingress_packets(frames, offset=0, flags=L.VERIFY_EVIL_BIT)
         want_v = np.array([O.ingress_verdict(f[:-4] if len(f) >= 4 else b"", O.VERIFY_EVIL_BIT) for f in frames],
@@ -100,7 +106,7 @@ def test_ingress_packets_gather(cuda):
     frames.append(_with_fcs(bytes(rng.integers(0, 256, cap - offset - 4, dtype=np.uint8))))  # fills the slot
     bufs = [b"\xAA" * offset + f for f in frames]
     assert max(len(b) for b in bufs) == cap
-    ring = L.RxRing(600, slot_cap=cap, batch_slots=100, depth=3)
+    ring = _ring(600, slot_cap=cap, batch_slots=100, depth=3)
     try:
         ok, verdict = ring.ingress_packets(bufs, offset=offset)
     finally:
@@ -113,7 +119,7 @@ def test_ingress_packets_gather(cuda):
 
 @pytest.mark.gpu
 def test_ingress_packets_rejects_oversize(cuda):
-    ring = L.RxRing(8, slot_cap=64)
+    ring = _ring(8, slot_cap=64)
     try:
         with pytest.raises(L.LnetoError):
             ring.ingress_packets([b"x" * 65])
@@ -126,7 +132,7 @@ def test_ring_mtu_batch_roundtrip(cuda):
     """64 Ki x 1500-byte frames with FCS through the pipelined ring: all pass;
     then one flipped byte per 1000 frames fails exactly those frames."""
     n, flen = 1 << 16, 1500
-    ring = L.RxRing(n, slot_cap=1536, batch_slots=8192, depth=3)
+    ring = _ring(n, slot_cap=1536, batch_slots=8192, depth=3)
     try:
         rng = np.random.default_rng(1)
         data = rng.integers(0, 256, (n, flen - 4), dtype=np.uint8)
@@ -156,7 +162,7 @@ def test_ingress_packets_fewer_slots_than_stages(cuda, nslots):
     """A ring with fewer slots than pipeline stages (depth 3) gathers into its
     own slots only (the stage block used to run past the pool)."""
     frames = _case_frames(seed=40 + nslots, count=37)
-    ring = L.RxRing(nslots, slot_cap=_cap_for(frames, 0), depth=3)
+    ring = _ring(nslots, slot_cap=_cap_for(frames, 0), depth=3)
     try:
         ok, verdict = ring.ingress_packets(frames, offset=0)
     finally:
@@ -183,7 +189,7 @@ def test_egress_packets_matches_oracle(cuda, flags):
         b[offset:offset + len(f)] = np.frombuffer(f, dtype=np.uint8)
         bufs.append(b)
     before = [b.copy() for b in bufs]
-    ring = L.RxRing(300, slot_cap=cap, batch_slots=128, depth=3)
+    ring = _ring(300, slot_cap=cap, batch_slots=128, depth=3)
     try:
         sizes, status = ring.egress_packets(bufs, [len(f) for f in frames], offset=offset, capacity=cap,
                                             flags=flags)
@@ -211,7 +217,7 @@ def test_ring_icmp_flag(cuda):
     messages; the flag travels through the ring's stages to the verdict kernel."""
     frames = [_with_fcs(f) for f in G.icmp_frames(seed=21, count=1200)]
     flags = L.VERIFY_ICMP | L.VERIFY_EVIL_BIT
-    ring = L.RxRing(400, slot_cap=_cap_for(frames, 0), batch_slots=100, depth=3)
+    ring = _ring(400, slot_cap=_cap_for(frames, 0), batch_slots=100, depth=3)
     try:
         ok, verdict = ring.ingress_packets(frames, offset=0, flags=flags)
     finally:
@@ -243,7 +249,7 @@ def test_ring_without_fcs(cuda, dense):
     offset = 2
     cap = _cap_for(frames, offset)
     for how in ("slots", "packets"):
-        ring = L.RxRing(len(frames), slot_cap=cap, batch_slots=256, depth=3)
+        ring = _ring(len(frames), slot_cap=cap, batch_slots=256, depth=3)
         try:
             if how == "slots":
                 _fill_ring(ring, frames, offset)
@@ -270,7 +276,7 @@ def test_ring_filter_precedence(cuda, no_fcs):
     frames = G.filter_frames(seed=91, count=1800)
     bufs = frames if no_fcs else [_with_fcs(f) for f in frames]
     flags = L.VERIFY_ICMP | (L.RX_NO_FCS if no_fcs else 0)
-    ring = L.RxRing(len(bufs), slot_cap=_cap_for(bufs, 0), batch_slots=512, depth=2)
+    ring = _ring(len(bufs), slot_cap=_cap_for(bufs, 0), batch_slots=512, depth=2)
     try:
         ring.set_filter(cfilt)
         ok, verdict = ring.ingress_packets(bufs, offset=0, flags=flags)
@@ -305,7 +311,7 @@ def test_ring_packed_zipf_lengths(cuda):
         if i % 501 == 0:
             f = b""
         frames.append(f)
-    ring = L.RxRing(len(frames), slot_cap=1536, batch_slots=1024, depth=3)
+    ring = _ring(len(frames), slot_cap=1536, batch_slots=1024, depth=3)
     try:
         _fill_ring(ring, frames, 0)
         ok, verdict = ring.ingress(0, len(frames))
@@ -322,3 +328,47 @@ def _flip(f: bytes, i: int) -> bytes:
     b = bytearray(f)
     b[i] ^= 0x08
     return bytes(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 8, 63, 64, 200])
+def test_host_threshold_paths_agree(cuda, n):
+    """Batches below the host threshold (LNX_HOST_BATCH_DEFAULT) run on the
+    host with no launch, the others on the GPU; both equal the oracle, for
+    ingress_packets, ring slots and egress_packets (netdev's Runner calls with
+    n = 1, x/netdev/runner.go:432-433)."""
+    frames = _case_frames(seed=900 + n, count=n)
+    want_ok, want_v = _expect(frames)
+    cap = 1536
+    for thr, where in ((L.HOST_BATCH_DEFAULT, "host" if n < L.HOST_BATCH_DEFAULT else "device"), (0, "device")):
+        ring = L.RxRing(max(n, 1), slot_cap=cap, batch_slots=128, depth=2, host_threshold=thr)
+        try:
+            s0 = ring.stats()
+            ok, verdict = ring.ingress_packets(frames)
+            assert (ok == want_ok).all() and (verdict == want_v).all(), (thr, n)
+            for i, f in enumerate(frames):
+                ring.slots[i, :len(f)] = np.frombuffer(f, np.uint8)
+                ring.lengths[i] = len(f)
+            ok2, verdict2 = ring.ingress(0, n)
+            assert (ok2 == want_ok).all() and (verdict2 == want_v).all(), (thr, n)
+            s1 = ring.stats()
+            if where == "host":
+                assert s1["device_batches"] == s0["device_batches"] and s1["host_frames"] - s0["host_frames"] == 2 * n
+            else:
+                assert s1["device_batches"] > s0["device_batches"] and s1["device_frames"] - s0["device_frames"] == 2 * n
+            # egress: the same frames (FCS stripped) finished in place, checked against the oracle
+            bufs = [np.zeros(cap, dtype=np.uint8) for _ in frames]
+            sizes = []
+            for b, f in zip(bufs, frames):
+                body = f[:-4] if len(f) >= 4 else f
+                b[:len(body)] = np.frombuffer(body, np.uint8)
+                sizes.append(len(body))
+            lens, status = ring.egress_packets(bufs, sizes, offset=0, capacity=cap)
+            for k, f in enumerate(frames):
+                body = f[:-4] if len(f) >= 4 else f
+                g, st = O.tx_checksum(body)
+                fin, st2 = O.fcs_append(g, cap)
+                assert int(status[k]) == (st or st2) and int(lens[k]) == len(fin), (thr, k)
+                assert bufs[k][:len(fin)].tobytes() == fin, (thr, k)
+        finally:
+            ring.close()
