@@ -367,7 +367,7 @@ def main():
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32",
                     choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search",
-                             "tx_checksum", "egress_packets", "ingress_packets"])
+                             "tx_checksum", "egress_packets", "ingress_packets", "rx_verify"])
     ap.add_argument("--short-frames", action="store_true",
                     help="--op crc32 / fcs_verify through lnx_*_batch_ex(LNX_BATCH_SHORT_FRAMES): the staged "
                          "lane-stream kernel the caller picks for a short-frame mix (DESIGN.md §3.9)")
@@ -478,7 +478,7 @@ def main():
         fcs = L.crc32_segments(d_bytes, starts, lens)
         fr[:, flen - 4:] = fcs.view(torch.uint8).view(n_local, 4)
         d_hit = torch.empty(n_local, dtype=torch.int64, device=dev)
-    elif args.op in ("ingress", "tx_checksum"):
+    elif args.op in ("ingress", "tx_checksum", "rx_verify"):
         if flen is None or flen < 42:
             raise SystemExit(f"--op {args.op} needs fixed-size frames of at least 42 bytes")
         fr = d_bytes[: n_local * flen].view(n_local, flen)
@@ -487,6 +487,7 @@ def main():
             + bytes.fromhex("14e90035") + (flen - 34).to_bytes(2, "big")
         fr[:, : len(hdr)] = torch.tensor(list(hdr), dtype=torch.uint8, device=dev)
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+        d_verdict = torch.empty(n_local, dtype=torch.uint8, device=dev)
         if args.op == "tx_checksum":
             # TX: the same frames as segments (start, len); the step writes the IPv4
             # header CRC and the UDP CRC in place, idempotently, every step
@@ -507,6 +508,8 @@ def main():
             L.fcs_verify_batch(d_bytes, d_off, out=d_ok, stream=stream, short_frames=args.short_frames)
         elif args.op == "ingress":
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
+        elif args.op == "rx_verify":
+            L.rx_verify_batch(d_bytes, d_off, out=(d_ok, d_verdict), stream=stream)
         elif args.op == "tx_checksum":
             L.tx_checksum_batch(d_bytes, d_seg, d_len, status=d_ok, stream=stream)
         elif args.op == "search":
@@ -580,6 +583,7 @@ def main():
         "fcs_verify": "GiB/s FCS verify (CRC-32 residue) over device-resident frames; % of HBM3E read peak",
         "sum16": "GiB/s RFC 791 internet checksum over device-resident segments; % of HBM3E read peak",
         "ingress": "GiB/s receive-path checksum verdicts (IPv4 header + UDP) over device-resident frames",
+        "rx_verify": "GiB/s receive check in one pass (FCS residue + IPv4 header / UDP verdicts) over device-resident frames",
         "search": "GiB/s CRC32Search over device-resident captures (bytes scanned to the FCS hit)",
         "fcs_append": "GiB/s TX FCS append (pad, CRC-32, LE32 store) over device-resident ring slots",
         "tx_checksum": "GiB/s TX checksum generate (IPv4 header + UDP) over device-resident frames",
@@ -622,6 +626,7 @@ def main():
                                       "each slice folded by the kernel slice_kind gives it, DESIGN.md §3.10)",
                              "fcs_verify": "lnx::crc32_rows_kernel<kVerify> + lnx::crc32_stage_kernel<kVerify>",
                        "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
+                       "rx_verify": "lnx::rx_verify_kernel<true, false>",
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
                        "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
@@ -686,6 +691,8 @@ def main():
             seeds = d_seed.cpu().numpy().view(np.uint32)
         elif args.op in ("fcs_verify", "ingress", "tx_checksum"):
             got = d_ok.cpu().numpy()
+        elif args.op == "rx_verify":
+            got = d_ok.cpu().numpy() * 256 + d_verdict.cpu().numpy()
         elif args.op == "search":
             got = d_hit.cpu().numpy()
         elif args.op == "fcs_append":
@@ -707,6 +714,8 @@ def main():
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
             elif args.op == "ingress":
                 want = O.ingress_verdict(fr)
+            elif args.op == "rx_verify":
+                want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C) * 256 + O.ingress_verdict(fr[:-4] if len(fr) >= 4 else b"")
             elif args.op == "tx_checksum":
                 # the finished frame is a fixed point of the step and passes the receive path
                 regen, st = O.tx_checksum(fr)

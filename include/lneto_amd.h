@@ -250,6 +250,17 @@ typedef struct lnx_rx_filter {  /* (EtherTypes must be > 1500: RegisterEthernet,
 int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                                       const lnx_rx_filter* filter, uint8_t* d_verdict, void* stream);
 
+/* lneto's whole receive check in ONE pass over each frame:
+ * for every frame d_bytes[d_off[i] : d_off[i+1]] carrying its 4-byte LE FCS,
+ * d_fcs_ok[i] = the FCS test of lnx_fcs_verify_batch and d_verdict[i] = the
+ * verdict lnx_ingress_verify_batch_filtered gives the frame without its FCS
+ * (flags LNX_VERIFY_EVIL_BIT / LNX_VERIFY_ICMP, filter NULL = accept-all).
+ * With LNX_RX_NO_FCS (a device that strips the FCS) no CRC is taken,
+ * d_fcs_ok[i] = 1 and the verdict covers the whole frame.  The receive ring
+ * runs it for its batches. */
+int lnx_rx_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                        const lnx_rx_filter* filter, uint8_t* d_fcs_ok, uint8_t* d_verdict, void* stream);
+
 /* Host-memory convenience: copies h_bytes/h_off to the device, runs
  * lnx_crc32_batch, copies the CRCs back, synchronously.  Used to measure the
  * PCIe-inclusive rate.  nbytes is the length of h_bytes; every

@@ -21,7 +21,7 @@ import os
 __all__ = [
     "LnetoError", "lib", "crc32", "crc32_update", "crc32_search", "sum_write_even", "sum16",
     "payload_sum16", "never_zero_sum", "CRC791", "crc32_batch", "fcs_verify_batch", "sum16_batch",
-    "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "device_count", "version", "build_id", "LIB_PATH",
+    "crc32_batch_host", "crc32_batch_multi", "tx_checksum_batch", "rx_verify_batch", "device_count", "version", "build_id", "LIB_PATH",
     "CRC32_RESIDUE", "RxRing", "RxFilter", "RX_NO_FCS", "research_lib",
 ]
 
@@ -129,6 +129,13 @@ _sig = {
     "lnx_fcs_verify_batch_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp]),
     "lnx_egress_packets": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32, _vp]),
+    "lnx_rx_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(RxFilter),
+                                            _vp, _vp, _vp]),
+    "lnx_ingress_verdict": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.POINTER(RxFilter)]),
+    "lnx_tx_checksum": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "lnx_fcs_append": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
+    "lnx_rx_ring_set_host_threshold": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+    "lnx_rx_ring_stats": (ctypes.c_int, [_vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
     "lnx_last_error": (ctypes.c_char_p, []),
     "lnx_version": (ctypes.c_char_p, []),
@@ -435,6 +442,26 @@ def ingress_verify_batch(d_bytes, d_off, flags: int = 0, out=None, stream=None, 
                                                            ctypes.byref(filter), out.data_ptr(), s)
             _check(rc, what)
     return out
+
+
+def rx_verify_batch(d_bytes, d_off, flags: int = 0, filter: RxFilter | None = None, out=None, stream=None):
+    """lneto's whole receive check in one pass over each frame (lnx_rx_verify_batch):
+    returns (fcs_ok, verdict) uint8 tensors — the FCS residue test of every frame
+    d_bytes[d_off[i]:d_off[i+1]] (FCS included) and the verdict of the frame
+    without its FCS.  flags: VERIFY_EVIL_BIT | VERIFY_ICMP | RX_NO_FCS."""
+    import torch
+    what = "lnx_rx_verify_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
+    n = d_off.numel() - 1
+    ok, verdict = out if out is not None else (None, None)
+    ok = _out(what, ok, n, torch.uint8, "u8", b.device)
+    verdict = _out(what, verdict, n, torch.uint8, "u8", b.device)
+    if n > 0:
+        with b as s:
+            _check(lib.lnx_rx_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, flags,
+                                           ctypes.byref(filter) if filter is not None else None, ok.data_ptr(),
+                                           verdict.data_ptr(), s), what)
+    return ok, verdict
 
 
 def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):

@@ -32,6 +32,9 @@ uint64_t crc32_launch_waves(uint64_t n, int num_cus);
 hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* len, const uint32_t* crc, uint64_t n,
                               uint32_t capacity, uint8_t* status, int num_cus, hipStream_t stream);
 #endif
+hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
+                            uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
+                            const uint32_t* image, int num_cus, hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
                                  uint32_t trim, const RxFilter* filter);
@@ -153,6 +156,23 @@ std::vector<uint32_t> build_stage_image() {
   return t;
 }
 
+// The fused receive kernel's image (rx_verify_kernel.hip): the slicing tables
+// T_k[e] = Z_128(e << 8k), T_{4+k}[e] = Z_124(e << 8k) (k < 4), then the nibble
+// tables of Z_{-8q} (q < 32) and Z_{-b} (b < 8), entry (t, i, v) at 128 t + 16 i + v.
+std::vector<uint32_t> build_rx_image() {
+  std::vector<uint32_t> t(2048 + 40 * 128);
+  for (uint32_t k = 0; k < 4; ++k)
+    for (uint32_t e = 0; e < 256; ++e) {
+      t[256 * k + e] = zshift_bytes(e << (8 * k), 128);
+      t[256 * (4 + k) + e] = zshift_bytes(e << (8 * k), 124);
+    }
+  for (uint32_t q = 0; q < 40; ++q)
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v)
+        t[2048 + 128 * q + 16 * i + v] = zshift_bytes(v << (4 * i), q < 32 ? -8 * (int64_t)q : -(int64_t)(q - 32));
+  return t;
+}
+
 // Tables of crc32_search_kernel: the byte-step table, then Z_{4*2^k} as four
 // byte tables for k = 0..5 (search_kernel.hip).
 // Then the tables of crc32_search_seg_kernel (24-byte lane segments): the
@@ -216,6 +236,7 @@ struct DeviceCtx {
   int num_cus = 0;
   uint32_t* d_search = nullptr;  // crc32_search_kernel tables
   uint32_t* d_stage = nullptr;   // crc32_stage_kernel image
+  uint32_t* d_rx = nullptr;      // rx_verify_kernel image
   // Per stream: the staged kernel's giant-slice slots (stage_kernel.hip
   // giant_pieces; zero between launches).  Launches on one stream run in
   // order, so each stream owns one set; streams never share one.
@@ -283,9 +304,11 @@ int init_ctx(DeviceCtx& c, int dev) {
     (void)hipFree(c.d_image);
     (void)hipFree(c.d_search);
     (void)hipFree(c.d_stage);
+    (void)hipFree(c.d_rx);
     c.d_image = nullptr;
     c.d_search = nullptr;
     c.d_stage = nullptr;
+    c.d_rx = nullptr;
     return hip_fail(err, what);
   };
   hipError_t err = hipDeviceGetAttribute(&c.num_cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -304,6 +327,11 @@ int init_ctx(DeviceCtx& c, int dev) {
     return fail(err, "hipMalloc(stage image)");
   if ((err = hipMemcpy(c.d_stage, sg.data(), sg.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
     return fail(err, "hipMemcpy(stage image)");
+  const std::vector<uint32_t> rx = build_rx_image();
+  if ((err = hipMalloc(reinterpret_cast<void**>(&c.d_rx), rx.size() * 4)) != hipSuccess)
+    return fail(err, "hipMalloc(rx image)");
+  if ((err = hipMemcpy(c.d_rx, rx.data(), rx.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail(err, "hipMemcpy(rx image)");
   return LNX_OK;
 }
 
@@ -385,13 +413,14 @@ int crc_common(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* 
 
 // For the other translation units (rx_ring.hip): the current device's LDS
 // image and CU count, and the thread's lnx_last_error.
-int device_resources(const void** image, int* num_cus, const void** stage_image) {
+int device_resources(const void** image, int* num_cus, const void** stage_image, const void** rx_image) {
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   *image = c->d_image;
   *num_cus = c->num_cus;
   if (stage_image) *stage_image = c->d_stage;
+  if (rx_image) *rx_image = c->d_rx;
   return LNX_OK;
 }
 int hip_error(hipError_t e, const char* what) { return hip_fail(e, what); }
@@ -552,6 +581,23 @@ int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_
   hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP), d_verdict,
                                        c->num_cus, static_cast<hipStream_t>(stream), nullptr, 0, &filt);
   if (e != hipSuccess) return hip_fail(e, "ingress_verify_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_rx_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
+                        const lnx_rx_filter* filter, uint8_t* d_fcs_ok, uint8_t* d_verdict, void* stream) {
+  RxFilter filt;
+  if (!rx_filter_of(filter, &filt)) return LNX_EINVAL;
+  if (flags & ~(uint32_t)(LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP | LNX_RX_NO_FCS)) return LNX_EINVAL;
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_fcs_ok || !d_verdict) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  const hipError_t e = launch_rx_verify(d_bytes, d_off, n, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP),
+                                        !(flags & LNX_RX_NO_FCS), d_fcs_ok, d_verdict, nullptr, &filt, c->d_rx,
+                                        c->num_cus, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "rx_verify_kernel launch");
   return LNX_OK;
 }
 

@@ -46,9 +46,10 @@
 
 namespace lnx {
 
-int device_resources(const void** image, int* num_cus, const void** stage_image);
-int crc_offsets(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void* d_out, bool verify, uint32_t policy,
-                hipStream_t stream);
+int device_resources(const void** image, int* num_cus, const void** stage_image, const void** rx_image);
+hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
+                            uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
+                            const uint32_t* image, int num_cus, hipStream_t stream);
 int hip_error(hipError_t e, const char* what);
 // host_path.cpp: the per-frame host forms (batches below the ring's host threshold)
 uint8_t host_verdict(const uint8_t* fr, size_t L, uint32_t flags, const RxFilter& f);
@@ -109,7 +110,8 @@ struct lnx_rx_ring {
   uint32_t host_below = LNX_HOST_BATCH_DEFAULT;
   lnx_rx_ring_counters stats{};  // lnx_rx_ring_stats (RunnerStatistics-style, x/netdev/runner.go:107-140)
   const void* image = nullptr;
-  const void* stage_image = nullptr;  // the staged lane streams' tables (short-frame batches)
+  const void* stage_image = nullptr;  // the staged lane streams' tables (unused since round 5)
+  const void* rx_image = nullptr;     // rx_verify_kernel's tables
   int num_cus = 0;
   std::mutex mu;  // one call at a time (the stages are shared)
 };
@@ -186,23 +188,15 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
   hipError_t e;
   const bool fcs = !(flags & LNX_RX_NO_FCS);
   const uint32_t vflags = flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP);
-  const uint32_t trim = fcs ? 4u : 0u;
   if (pack) {
     const uint64_t total = s.h_off[nb];
     if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
         (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess)
       return hip_error(e, "rx ring H2D (packed)");
-    // the packed batch's FCS verify: lnx_fcs_verify_batch's dispatch (the
-    // rows or the staged kernel per slice)
-    if (!fcs) {
-      if ((e = hipMemsetAsync(s.d_ok, 1, nb, s.s)) != hipSuccess) return hip_error(e, "rx ring FCS verify memset");
-    } else {
-      const int rc = crc_offsets(s.d_bytes, s.d_start, nb, s.d_ok, true, 0u /* kPolicyAuto */, s.s);
-      if (rc != LNX_OK) return rc;
-    }
-    if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, nullptr, trim,
-                                   &r->filt)) != hipSuccess)
-      return hip_error(e, "rx ring ingress verify launch");
+    // FCS and verdicts in one pass over each frame (rx_verify_kernel.hip)
+    if ((e = launch_rx_verify(s.d_bytes, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, nullptr, &r->filt,
+                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring rx_verify launch");
   } else {
     const size_t cap = r->cap;
     if ((e = hipMemcpyAsync(s.d_bytes, r->h_slots + (size_t)b0 * cap, (size_t)nb * cap, hipMemcpyHostToDevice,
@@ -212,12 +206,9 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
     const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
     hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
     if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
-    e = fcs ? launch_fcs_verify_segments(s.d_bytes, s.d_start, s.d_len, nb, s.d_ok, r->image, r->num_cus, s.s)
-            : hipMemsetAsync(s.d_ok, 1, nb, s.s);
-    if (e != hipSuccess) return hip_error(e, "rx ring FCS verify launch");
-    if ((e = launch_ingress_verify(s.d_bytes, s.d_start, nb, vflags, s.d_verdict, r->num_cus, s.s, s.d_len, trim,
-                                   &r->filt)) != hipSuccess)
-      return hip_error(e, "rx ring ingress verify launch");
+    if ((e = launch_rx_verify(s.d_bytes, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, s.d_len, &r->filt,
+                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring rx_verify launch");
   }
   if ((e = hipMemcpyAsync(ok_dst, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(verdict_dst, s.d_verdict, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess)
@@ -297,7 +288,7 @@ int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t 
   if (e != hipSuccess) return hip_error(e, "hipSetDevice");
   auto* r = new lnx_rx_ring;
   r->device = device, r->nslots = nslots, r->cap = slot_cap, r->batch = batch_slots, r->depth = depth;
-  int rc = device_resources(&r->image, &r->num_cus, &r->stage_image);
+  int rc = device_resources(&r->image, &r->num_cus, &r->stage_image, &r->rx_image);
   if (rc != LNX_OK) { ring_free(r); return rc; }
   const size_t slots_bytes = (size_t)nslots * slot_cap;
   if ((e = hipHostMalloc(reinterpret_cast<void**>(&r->h_slots), slots_bytes, hipHostMallocDefault)) != hipSuccess ||

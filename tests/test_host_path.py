@@ -16,12 +16,12 @@ from tests.test_rx_filter import FILTERS, _pair
 
 import lneto_amd as L
 
-L.lib.lnx_ingress_verdict.restype = ctypes.c_int
-L.lib.lnx_ingress_verdict.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p]
-L.lib.lnx_tx_checksum.restype = ctypes.c_int
-L.lib.lnx_tx_checksum.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-L.lib.lnx_fcs_append.restype = ctypes.c_int
-L.lib.lnx_fcs_append.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
+
+
+
+
+
+
 
 
 def _verdict(frame: bytes, flags: int = 0, filt=None) -> int:
