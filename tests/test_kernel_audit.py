@@ -38,7 +38,7 @@ def test_every_kernel_instantiation_passes_the_ring_audit(tmp_path, build):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
-@pytest.mark.parametrize("src", ["crc32_kernel", "stage_kernel", "stage_research", "sum16_kernel", "ingress_kernel",
+@pytest.mark.parametrize("src", ["crc32_kernel", "stage_kernel", "stage_research", "sum16_kernel", "ingress_kernel", "rx_verify_kernel",
                                  "search_kernel", "rx_ring"])
 @pytest.mark.parametrize("build", ["product", "research"])
 def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
