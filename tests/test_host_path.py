@@ -17,13 +17,6 @@ from tests.test_rx_filter import FILTERS, _pair
 import lneto_amd as L
 
 
-
-
-
-
-
-
-
 def _verdict(frame: bytes, flags: int = 0, filt=None) -> int:
     return L.lib.lnx_ingress_verdict(frame, len(frame), flags, ctypes.byref(filt) if filt is not None else None)
 
