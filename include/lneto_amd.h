@@ -362,7 +362,11 @@ int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uin
  * Synchronous; the batches are pipelined over the ring's stages (gather, H2D,
  * kernels, D2H, scatter), nothing is retained after the call.  Frames travel
  * packed back to back, each with room for its padding and FCS only.  On an
- * error return, lens and status are left as they were and no buffer is written. */
+ * error return the frames of batches that completed before the error may
+ * already be written back (with their lens and status); the failing batch's
+ * and later frames, lens and status are left as they were, and every stage has
+ * drained before the call returns.  lnx_ingress_packets writes results the
+ * same way. */
 #define LNX_TX_CHECKSUM 1u
 #define LNX_TX_FCS 2u
 int lnx_egress_packets(lnx_rx_ring* ring, uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset,

@@ -183,6 +183,14 @@ uint64_t pack_batch(Stage& s, uint32_t nb, Ptr ptr, Len len) {
 // (offsets s.h_off[0..nb]); else they sit in whole slots [b0, b0 + nb) of the
 // ring at `offset`.  FCS verify unless LNX_RX_NO_FCS (then fcs_ok = 1 and the
 // verdict covers the whole frame).
+// After a failed call: wait for whatever a part-way enqueue left on every
+// stage's stream (async copies out of / into the staging), so the next call may
+// repack the staging.  Errors here are the failed call's, already reported.
+void quiesce(lnx_rx_ring* r) {
+  for (auto& s : r->st)
+    if (s.s) (void)hipStreamSynchronize(s.s);
+}
+
 int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, uint32_t offset, uint32_t flags,
                uint8_t* ok_dst, uint8_t* verdict_dst) {
   hipError_t e;
@@ -449,6 +457,7 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
     const int d = drain(k);
     if (rc == LNX_OK) rc = d;
   }
+  if (rc != LNX_OK) quiesce(r);
   return rc;
 }
 
@@ -527,6 +536,7 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     const int d = drain(k);
     if (rc == LNX_OK) rc = d;
   }
+  if (rc != LNX_OK) quiesce(r);
   return rc;
 }
 
