@@ -5,4 +5,5 @@ timeout -k 10 180 python -u bench.py --steps 50 --warmup 5 --no-cpu-baseline --n
 timeout -k 10 180 python -u bench.py --steps 50 --warmup 5 --op rx_verify --no-cpu-baseline --verify > gpurun_out/r5b_bench_rx_verify.jsonl 2>&1 &&
 timeout -k 10 180 python -u bench.py --steps 20 --warmup 3 --workload zipf64_1500 --no-cpu-baseline > gpurun_out/r5b_bench_zipf.jsonl 2>&1 &&
 timeout -k 10 180 python -u bench.py --steps 20 --warmup 3 --workload zipf64_1500 --short-frames --no-cpu-baseline > gpurun_out/r5b_bench_zipf_short.jsonl 2>&1 &&
-timeout -k 10 180 python -u bench.py --steps 50 --warmup 3 --workload jumbo9000 --no-cpu-baseline > gpurun_out/r5b_bench_jumbo.jsonl 2>&1
+timeout -k 10 180 python -u bench.py --steps 50 --warmup 3 --workload jumbo9000 --no-cpu-baseline > gpurun_out/r5b_bench_jumbo.jsonl 2>&1 &&
+timeout -k 10 300 ./tools/ubench/call_latency > gpurun_out/r5b_call_latency.jsonl 2>&1
