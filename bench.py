@@ -193,7 +193,9 @@ def rx_ring_bench(args, L, synth, torch, dev, world):
     host = d.cpu().numpy()
     del d, pos
     ring = L.RxRing(n, slot_cap=cap, batch_slots=args.ring_batch, depth=args.ring_depth)
+    zero_copy = not args.ring_copy
     try:
+        ring.set_zero_copy(zero_copy)
         # slot i = frame i at offset 0
         if zipf:
             slots = ring.slots
@@ -215,16 +217,20 @@ def rx_ring_bench(args, L, synth, torch, dev, world):
     batches = -(-n // args.ring_batch)
     fill = nbytes / (n * cap)
     packed = fill < 0.9  # the ring's rule (rx_ring.hip lnx_rx_ring_ingress)
-    h2d = nbytes + 8 * (n + batches) if packed else n * cap + 4 * n
+    if zero_copy:  # the kernel reads the frame bytes in place; DMA moves only the lengths
+        h2d, copy = nbytes + 4 * n, "zero copy (kernel reads the pinned slots; lengths by DMA)"
+    else:
+        h2d = nbytes + 8 * (n + batches) if packed else n * cap + 4 * n
+        copy = "packed (frames + offsets)" if packed else "whole slots"
     out = {
-        "metric": "GiB/s receive ring, PCIe-inclusive (pinned slots -> H2D -> FCS verify + ingress verdicts -> D2H)",
+        "metric": "GiB/s receive ring, PCIe-inclusive (pinned slots -> FCS verify + ingress verdicts -> D2H)",
         "value": round(nbytes / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic {'Zipf 64-1500 B' if zipf else '1500-byte'} frames with valid FCS in {cap}-byte slots",
         "config": {"workload": f"1M {'Zipf-mix' if zipf else 'x 1500 B'} frames in host memory", "frames": n,
                    "frame_bytes": nbytes, "slot_cap": cap, "slot_fill": round(fill, 4),
-                   "copy": "packed (frames + offsets)" if packed else "whole slots",
+                   "copy": copy,
                    "pcie_bytes_per_step": h2d, "pcie_d2h_bytes_per_step": 2 * n,
                    "pcie_bytes_per_frame_byte": round(h2d / nbytes, 4),
                    "depth": args.ring_depth, "batch_slots": args.ring_batch, "kernel": L.version()},
@@ -268,9 +274,19 @@ def packets_bench(args, L, synth, torch, dev, world):
     zipf = args.workload == "zipf64_1500"
     wire = synth.zipf_lengths(n).astype(np.int64) if zipf else np.full(n, FRAME_BYTES, dtype=np.int64)
     rows = _udp4_frames(synth, n, cap, wire)
+    slot_bufs = args.bufs == "slots"
+    if slot_bufs:
+        # RunnerConfig.Buffers carved from the ring's slots (x/netdev/runner.go:92-94): the
+        # kernels read (egress: patch) the frames in place
+        ring = L.RxRing(n, slot_cap=cap, batch_slots=args.ring_batch, depth=args.ring_depth)
+        ring.slots[:] = rows
+        del rows
+        rows = ring.slots
+    else:
+        ring = L.RxRing(args.ring_batch, slot_cap=cap,  # (the packet calls stage through the ring)
+                        batch_slots=args.ring_batch, depth=args.ring_depth)
+    ring.set_zero_copy(not args.ring_copy)
     ptrs = (rows.ctypes.data + cap * np.arange(n, dtype=np.uint64)).astype(np.uint64)
-    ring = L.RxRing(args.ring_batch, slot_cap=cap,  # (the packet calls stage through the ring; its slots stay unused)
-                    batch_slots=args.ring_batch, depth=args.ring_depth)
     status = np.zeros(n, dtype=np.uint8)
     verdict = np.zeros(n, dtype=np.uint8)
     try:
@@ -287,9 +303,16 @@ def packets_bench(args, L, synth, torch, dev, world):
             step()
             assert (lens == wire.astype(np.uint32)).all() and (status == 0).all(), "egress: unexpected lengths/status"
             room = np.maximum(sizes0.astype(np.int64), 60) + 4
-            h2d = int(room.sum()) + 12 * n
-            d2h = int(room.sum()) + 6 * n
-            what = "gather -> H2D -> TX checksum generate + pad + FCS append -> D2H -> scatter"
+            zc = ring.stats()["zero_copy_frames"]
+            if zc:
+                assert zc == n, f"egress: {zc} of {n} frames zero-copy"
+                h2d = 2 * int(sizes0.sum()) + 12 * n  # both kernels read the frame in place
+                d2h = 6 * n  # (+ the in-place header / FCS stores)
+                what = "slot buffers in place: TX checksum generate + pad + FCS append on the pinned slots"
+            else:
+                h2d = int(room.sum()) + 12 * n
+                d2h = int(room.sum()) + 6 * n
+                what = "gather -> H2D -> TX checksum generate + pad + FCS append -> D2H -> scatter"
         else:
             # frames already finished by the transmit path: run egress once to give them checksums + FCS
             sizes0 = (wire - 4).astype(np.uint32)
@@ -304,11 +327,16 @@ def packets_bench(args, L, synth, torch, dev, world):
                                                status.ctypes.data, verdict.ctypes.data)
                 if rc != 0:
                     raise L.LnetoError(f"lnx_ingress_packets: {rc}")
+            z0 = ring.stats()["zero_copy_frames"]
             step()
             assert (status == 1).all() and (verdict == 0).all(), "ingress: valid frames not accepted"
-            h2d = int(wire.sum()) + 8 * (n + -(-n // args.ring_batch))
             d2h = 2 * n
-            what = "gather -> H2D -> FCS verify + receive verdicts -> D2H"
+            if ring.stats()["zero_copy_frames"] - z0 == n:
+                h2d = int(wire.sum()) + 12 * n
+                what = "slot buffers in place: frame table H2D -> FCS verify + receive verdicts -> D2H"
+            else:
+                h2d = int(wire.sum()) + 8 * (n + -(-n // args.ring_batch))
+                what = "gather -> H2D -> FCS verify + receive verdicts -> D2H"
         for _ in range(max(args.warmup, 1) - 1):
             step()
         t0 = time.perf_counter()
@@ -319,12 +347,12 @@ def packets_bench(args, L, synth, torch, dev, world):
         ring.close()
     nbytes = int(wire.sum())
     out = {
-        "metric": f"GiB/s {args.op} (per-frame pageable buffers: {what})",
+        "metric": f"GiB/s {args.op} ({'ring slot buffers' if slot_bufs else 'per-frame pageable buffers'}: {what})",
         "value": round(nbytes / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic UDP/IPv4 {'Zipf 64-1500 B' if zipf else '1500-byte'} frames (on the wire), "
-                f"one pageable {cap}-byte buffer each",
+                f"one {'pinned ring slot' if slot_bufs else 'pageable'} {cap}-byte buffer each",
         "config": {"workload": f"1M {'Zipf-mix' if zipf else 'x 1500 B'} frames in host memory", "frames": n,
                    "frame_bytes": nbytes, "pcie_h2d_bytes_per_step": h2d, "pcie_d2h_bytes_per_step": d2h,
                    "mpps": round(n / el / 1e6, 2), "depth": args.ring_depth, "batch_slots": args.ring_batch,
@@ -373,6 +401,10 @@ def main():
                          "lane-stream kernel the caller picks for a short-frame mix (DESIGN.md §3.9)")
     ap.add_argument("--ring-depth", type=int, default=3, help="--op rx_ring: pipeline stages")
     ap.add_argument("--ring-batch", type=int, default=65536, help="--op rx_ring: slots per stage batch")
+    ap.add_argument("--ring-copy", action="store_true",
+                    help="--op rx_ring / *_packets: copy frames through staging (lnx_rx_ring_set_zero_copy(0))")
+    ap.add_argument("--bufs", choices=["own", "slots"], default="own",
+                    help="--op *_packets: pageable buffers of the caller, or views of the ring's slots")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed launches for this long before the W warmup steps (GPU clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

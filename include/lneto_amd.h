@@ -318,8 +318,20 @@ typedef struct lnx_rx_ring_counters {
   uint64_t host_frames;
   uint64_t device_frames;
   uint64_t device_batches;
+  uint64_t zero_copy_frames;  /* of device_frames: read (and, egress, patched) in place in the slots */
 } lnx_rx_ring_counters;
 int lnx_rx_ring_stats(lnx_rx_ring* ring, lnx_rx_ring_counters* out);
+
+/* Zero copy (on by default): the ring's slots are mapped into the GPU's
+ * address space and the kernels read the frames in place over PCIe, so no host
+ * thread copies a frame and only frame bytes cross the link.  This covers
+ * lnx_rx_ring_ingress and, when every buffer of a batch lies in the ring's slot
+ * memory (netdev RunnerConfig.Buffers carved from lnx_rx_ring_slots,
+ * x/netdev/runner.go:92-94), lnx_ingress_packets and lnx_egress_packets (whose
+ * kernels then patch the frames in place: egress also needs the buffers in
+ * slot order).  Other buffers are gathered into pinned staging as before.
+ * on = 0 selects the copying forms for every batch. */
+int lnx_rx_ring_set_zero_copy(lnx_rx_ring* ring, int on);
 
 /* Device delivers frames without their FCS (x/netdev/interface.go:34-40 leaves
  * the FCS to "device or stack"): no FCS check (fcs_ok = 1), verdicts on the

@@ -279,7 +279,8 @@ class RxRing {
               bool evilBit = false) {
     return lnx_rx_ring_ingress(r_, first, count, offset, flags(evilBit), fcsOK, verdict);
   }
-  // Caller-owned buffers (gathered into pinned staging for the call only).
+  // Caller-owned buffers (gathered into pinned staging for the call only,
+  // read in place when they are the ring's slots: SlotBuffers).
   int IngressPackets(const uint8_t* const* bufs, const uint32_t* lens, uint64_t n, uint32_t offset, uint8_t* fcsOK,
                      uint8_t* verdict, bool evilBit = false) {
     return lnx_ingress_packets(r_, bufs, lens, n, offset, flags(evilBit), fcsOK, verdict);
@@ -315,6 +316,16 @@ class RxRing {
   }
   uint32_t Slots() const { return nslots_; }
   uint32_t SlotCap() const { return cap_; }
+  // The slots as netdev RunnerConfig.Buffers (x/netdev/runner.go:92-94): a
+  // Runner built on these hands IngressPackets / EgressPackets views of the
+  // ring's own pinned memory, which the kernels read (and patch) in place.
+  std::vector<lneto::Bytes> SlotBuffers() {
+    std::vector<lneto::Bytes> b;
+    for (uint32_t k = 0; k < nslots_; ++k) b.emplace_back(Slot(k), cap_);
+    return b;
+  }
+  // In-place access to the slots (default) or copies through staging.
+  int SetZeroCopy(bool on) { return lnx_rx_ring_set_zero_copy(r_, on ? 1 : 0); }
   // Batches below `frames` run on the host (no launch); 0 = always the GPU.
   int SetHostThreshold(uint32_t frames) { return lnx_rx_ring_set_host_threshold(r_, frames); }
   lnx_rx_ring_counters Stats() const {

@@ -136,6 +136,7 @@ _sig = {
     "lnx_fcs_append": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "lnx_rx_ring_set_host_threshold": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "lnx_rx_ring_stats": (ctypes.c_int, [_vp, _vp]),
+    "lnx_rx_ring_set_zero_copy": (ctypes.c_int, [_vp, ctypes.c_int]),
     "lnx_device_count": (ctypes.c_int, []),
     "lnx_last_error": (ctypes.c_char_p, []),
     "lnx_version": (ctypes.c_char_p, []),
@@ -559,10 +560,15 @@ class RxRing:
         _check(lib.lnx_rx_ring_set_host_threshold(self._h, frames), "lnx_rx_ring_set_host_threshold")
 
     def stats(self) -> dict:
-        """{host_frames, device_frames, device_batches} since creation (lnx_rx_ring_stats)."""
-        c = (ctypes.c_uint64 * 3)()
+        """{host_frames, device_frames, device_batches, zero_copy_frames} since creation (lnx_rx_ring_stats)."""
+        c = (ctypes.c_uint64 * 4)()
         _check(lib.lnx_rx_ring_stats(self._h, c), "lnx_rx_ring_stats")
-        return {"host_frames": c[0], "device_frames": c[1], "device_batches": c[2]}
+        return {"host_frames": c[0], "device_frames": c[1], "device_batches": c[2], "zero_copy_frames": c[3]}
+
+    def set_zero_copy(self, on: bool) -> None:
+        """Kernels read (egress: patch) frames in place in the pinned slots (the default), or
+        copy them through staging (lnx_rx_ring_set_zero_copy)."""
+        _check(lib.lnx_rx_ring_set_zero_copy(self._h, int(bool(on))), "lnx_rx_ring_set_zero_copy")
 
     def set_filter(self, filt: RxFilter | None) -> None:
         """The ring's stack configuration (lnx_rx_ring_set_filter); None = accept-all."""

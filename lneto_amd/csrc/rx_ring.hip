@@ -23,13 +23,20 @@
 // so the copy of batch k+1 overlaps the kernels of batch k: the pipeline runs
 // at the PCIe rate, the kernels are ~100x faster than the link.
 //
-// PCIe bytes: a batch whose frames fill under 90 % of their slots (a realistic
-// length mix: the Zipf mix averages 246 B in 1536-B slots, 6.2x) is packed back
-// to back on the host into the stage's pinned staging with n + 1 offsets, and
-// the kernels run in offsets mode, so the H2D carries the frame bytes plus 8
-// bytes per frame.  lnx_ingress_packets always packs (it gathers the caller's
-// buffers anyway); lnx_egress_packets packs each frame with room for its
-// padding and FCS only, and copies back just that.
+// Zero copy (round 5, the default): the slots are mapped into the GPU's
+// address space, so the receive kernel reads each frame straight from the
+// pinned slot over PCIe (only the frame's bytes cross the link, whatever the
+// slot fill) and no host thread copies a frame.  A batch then costs the H2D of
+// its lengths (4 B per frame), ring_segments_kernel, rx_verify_kernel and the
+// D2H of 2 B of results per frame.  lnx_ingress_packets / lnx_egress_packets
+// take the same path when the caller's buffers are the ring's slots (netdev's
+// RunnerConfig.Buffers, x/netdev/runner.go:92-94, can be exactly those: see
+// INTEGRATION.md); the transmit kernels then patch the frames in place in host
+// memory.  Buffers elsewhere (pageable memory) are gathered back to back into
+// pinned staging (n + 1 offsets, so PCIe carries the frame bytes plus 8 bytes
+// per frame) and, for egress, scattered back.  lnx_rx_ring_set_zero_copy(0)
+// selects the copying forms for every batch (the round-4 path: whole slots when
+// they are at least 90 % full, else packed).
 //
 // Stack configuration (lnx_rx_ring_set_filter) and FCS-less devices
 // (LNX_RX_NO_FCS) follow the reference's receive path exactly
@@ -85,6 +92,8 @@ struct lnx_rx_ring {
   int device = 0;
   uint32_t nslots = 0, cap = 0, batch = 0, depth = 0;
   uint8_t* h_slots = nullptr;  // the producer's slots (lnx_rx_ring_slots)
+  uint8_t* d_slots = nullptr;  // the same memory as the GPU addresses it (hipHostGetDevicePointer)
+  bool zero_copy = true;       // lnx_rx_ring_set_zero_copy
   uint32_t* h_len = nullptr;
   uint8_t* h_ok = nullptr;     // per slot: lnx_rx_ring_ingress results
   uint8_t* h_verdict = nullptr;
@@ -178,11 +187,6 @@ uint64_t pack_batch(Stage& s, uint32_t nb, Ptr ptr, Len len) {
   return o;
 }
 
-// Receive direction on stage s (asynchronous), results into ok_dst /
-// verdict_dst (pinned, nb entries).  pack: the frames are packed in s.h_pack
-// (offsets s.h_off[0..nb]); else they sit in whole slots [b0, b0 + nb) of the
-// ring at `offset`.  FCS verify unless LNX_RX_NO_FCS (then fcs_ok = 1 and the
-// verdict covers the whole frame).
 // After a failed call: wait for whatever a part-way enqueue left on every
 // stage's stream (async copies out of / into the staging), so the next call may
 // repack the staging.  Errors here are the failed call's, already reported.
@@ -191,19 +195,57 @@ void quiesce(lnx_rx_ring* r) {
     if (s.s) (void)hipStreamSynchronize(s.s);
 }
 
-int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, uint32_t offset, uint32_t flags,
+// Where a batch's frames are for the device.
+enum class RxSrc {
+  kPacked,       // packed in s.h_pack, offsets s.h_off[0..nb] (copied up)
+  kSlotsCopy,    // whole slots [b0, b0 + nb) at `offset`, copied up
+  kSlotsDirect,  // slots [b0, b0 + nb) at `offset`, read in place (zero copy)
+  kSegDirect,    // frame j at ring byte s.h_off[j], s.h_len[j] bytes, read in place
+};
+
+// Whether buffer b (frame b[offset : offset + need]) lies inside the ring's
+// slot memory, and its byte position there.
+bool in_ring(const lnx_rx_ring* r, const uint8_t* b, uint64_t offset, uint64_t need, uint64_t* pos) {
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(r->h_slots), x = reinterpret_cast<uintptr_t>(b);
+  const uint64_t size = (uint64_t)r->nslots * r->cap;
+  if (x < lo || x - lo > size || offset + need > size - (x - lo)) return false;
+  *pos = (uint64_t)(x - lo) + offset;
+  return true;
+}
+
+// Receive direction on stage s (asynchronous), results into ok_dst /
+// verdict_dst (pinned, nb entries), frames as `src` says.  FCS verify unless
+// LNX_RX_NO_FCS (then fcs_ok = 1 and the verdict covers the whole frame).
+int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, RxSrc src, uint32_t b0, uint32_t offset, uint32_t flags,
                uint8_t* ok_dst, uint8_t* verdict_dst) {
   hipError_t e;
   const bool fcs = !(flags & LNX_RX_NO_FCS);
   const uint32_t vflags = flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP);
-  if (pack) {
+  const uint32_t* rx_image = static_cast<const uint32_t*>(r->rx_image);
+  if (src == RxSrc::kSegDirect) {
+    if ((e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)nb * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess ||
+        (e = hipMemcpyAsync(s.d_len, s.h_len, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring H2D (frame table)");
+    if ((e = launch_rx_verify(r->d_slots, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, s.d_len, &r->filt,
+                              rx_image, r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring rx_verify launch");
+  } else if (src == RxSrc::kSlotsDirect) {
+    if ((e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring H2D (lengths)");
+    const uint32_t grid = std::min<uint32_t>((nb + 255) / 256, 1024);
+    hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
+    if ((e = launch_rx_verify(r->d_slots + (size_t)b0 * r->cap, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict,
+                              s.d_len, &r->filt, rx_image, r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "rx ring rx_verify launch");
+  } else if (src == RxSrc::kPacked) {
     const uint64_t total = s.h_off[nb];
     if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
         (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)(nb + 1) * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess)
       return hip_error(e, "rx ring H2D (packed)");
     // FCS and verdicts in one pass over each frame (rx_verify_kernel.hip)
     if ((e = launch_rx_verify(s.d_bytes, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, nullptr, &r->filt,
-                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+                              rx_image, r->num_cus, s.s)) != hipSuccess)
       return hip_error(e, "rx ring rx_verify launch");
   } else {
     const size_t cap = r->cap;
@@ -215,7 +257,7 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
     hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
     if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
     if ((e = launch_rx_verify(s.d_bytes, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, s.d_len, &r->filt,
-                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+                              rx_image, r->num_cus, s.s)) != hipSuccess)
       return hip_error(e, "rx ring rx_verify launch");
   }
   if ((e = hipMemcpyAsync(ok_dst, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
@@ -226,13 +268,18 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, bool pack, uint32_t b0, ui
   return LNX_OK;
 }
 
-// Transmit direction on stage s (asynchronous): the nb frames packed in
-// s.h_pack at starts s.h_off[j] with lengths s.h_len[j] (each with room for
-// its padding and FCS) get their checksums (LNX_TX_CHECKSUM) and padding + FCS
-// (LNX_TX_FCS) on the device and come back with their new lengths; s.h_verdict
-// = the checksum status, s.h_ok = the append status.
-int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t capacity, uint32_t flags) {
+// Transmit direction on stage s (asynchronous): the nb frames at starts
+// s.h_off[j] with lengths s.h_len[j] (each with room for its padding and FCS)
+// get their checksums (LNX_TX_CHECKSUM) and padding + FCS (LNX_TX_FCS) on the
+// device and come back with their new lengths; s.h_verdict = the checksum
+// status, s.h_ok = the append status.  direct: the starts are ring bytes
+// past `base` and the kernels patch the frames in place in the slots (zero
+// copy); else they are packed in s.h_pack (total bytes) and copied both ways.
+int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t capacity, uint32_t flags,
+               bool direct = false, uint64_t base = 0) {
   hipError_t e;
+  uint8_t* bytes = direct ? r->d_slots + base : s.d_bytes;
+  if (direct) total = 0;
   if ((total && (e = hipMemcpyAsync(s.d_bytes, s.h_pack, total, hipMemcpyHostToDevice, s.s)) != hipSuccess) ||
       (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)nb * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(s.d_len, s.h_len, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
@@ -240,10 +287,10 @@ int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t c
   if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess || (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
     return hip_error(e, "tx ring status reset");
   if ((flags & LNX_TX_CHECKSUM) &&
-      (e = launch_tx_checksum(s.d_bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
+      (e = launch_tx_checksum(bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
     return hip_error(e, "tx ring checksum launch");
   if ((flags & LNX_TX_FCS) &&
-      (e = launch_fcs_append(s.d_bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
+      (e = launch_fcs_append(bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
           hipSuccess)
     return hip_error(e, "tx ring FCS append launch");
   if ((total && (e = hipMemcpyAsync(s.h_pack, s.d_bytes, total, hipMemcpyDeviceToHost, s.s)) != hipSuccess) ||
@@ -283,6 +330,13 @@ int lnx_rx_ring_set_host_threshold(lnx_rx_ring* r, uint32_t frames) {
   return LNX_OK;
 }
 
+int lnx_rx_ring_set_zero_copy(lnx_rx_ring* r, int on) {
+  if (!r) return LNX_EINVAL;
+  std::lock_guard<std::mutex> lk(r->mu);
+  r->zero_copy = on != 0;
+  return LNX_OK;
+}
+
 int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t batch_slots, uint32_t depth,
                        lnx_rx_ring** out) {
   if (!out) return LNX_EINVAL;
@@ -309,6 +363,11 @@ int lnx_rx_ring_create(int device, uint32_t nslots, uint32_t slot_cap, uint32_t 
     return rc;
   }
   std::memset(r->h_len, 0, (size_t)nslots * 4);
+  if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&r->d_slots), r->h_slots, 0)) != hipSuccess) {
+    rc = hip_error(e, "hipHostGetDevicePointer(rx ring slots)");
+    ring_free(r);
+    return rc;
+  }
   r->st.resize(depth);
   const size_t bb = (size_t)batch_slots * slot_cap;
   for (auto& s : r->st) {
@@ -377,6 +436,11 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
       const uint32_t l = std::min(r->h_len[b0 + j], r->cap);
       return l > offset ? l - offset : 0u;
     };
+    if (r->zero_copy) {  // frames read in place: no host copy, only frame bytes cross PCIe
+      rc = enqueue_rx(r, s, nb, RxSrc::kSlotsDirect, b0, offset, flags, r->h_ok + b0, r->h_verdict + b0);
+      if (rc == LNX_OK) r->stats.zero_copy_frames += nb;
+      continue;
+    }
     uint64_t total = 0;
     for (uint32_t j = 0; j < nb; ++j) total += flen(j);
     // whole slots when the frames fill them (no host copy); else frames packed
@@ -389,7 +453,8 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
       pack_batch(s, nb, [&](uint32_t j) { return r->h_slots + (size_t)(b0 + j) * r->cap + offset; }, flen);
     }
     packed_pending[k % r->depth] = pack;
-    rc = enqueue_rx(r, s, nb, pack, b0, offset, flags, r->h_ok + b0, r->h_verdict + b0);
+    rc = enqueue_rx(r, s, nb, pack ? RxSrc::kPacked : RxSrc::kSlotsCopy, b0, offset, flags, r->h_ok + b0,
+                    r->h_verdict + b0);
   }
   for (auto& s : r->st) {
     const hipError_t se = hipStreamSynchronize(s.s);
@@ -446,10 +511,19 @@ int lnx_ingress_packets(lnx_rx_ring* r, const uint8_t* const* bufs, const uint32
     if (rc != LNX_OK) break;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
     auto& s = r->st[sk];
-    pack_batch(
-        s, nb, [&](uint32_t j) { return bufs[i0 + j] + offset; },
-        [&](uint32_t j) -> uint64_t { return lens[i0 + j] > offset ? lens[i0 + j] - offset : 0u; });
-    rc = enqueue_rx(r, s, nb, true, 0, 0, flags, s.h_ok, s.h_verdict);
+    auto flen = [&](uint32_t j) -> uint32_t { return lens[i0 + j] > offset ? lens[i0 + j] - offset : 0u; };
+    // the caller's buffers are the ring's own slots (RunnerConfig.Buffers from
+    // lnx_rx_ring_slots): a frame table only, the kernel reads them in place
+    bool direct = r->zero_copy;
+    for (uint32_t j = 0; j < nb && direct; ++j) {
+      uint64_t pos = 0;  // (an empty frame reads nothing: any position)
+      direct = flen(j) == 0 || in_ring(r, bufs[i0 + j], offset, flen(j), &pos);
+      s.h_off[j] = pos;
+      s.h_len[j] = flen(j);
+    }
+    if (!direct) pack_batch(s, nb, [&](uint32_t j) { return bufs[i0 + j] + offset; }, flen);
+    rc = enqueue_rx(r, s, nb, direct ? RxSrc::kSegDirect : RxSrc::kPacked, 0, 0, flags, s.h_ok, s.h_verdict);
+    if (rc == LNX_OK && direct) r->stats.zero_copy_frames += nb;
     if (rc == LNX_OK) pending[sk] = {i0, nb};
   }
   for (uint32_t k = 0; k < depth; ++k) {
@@ -465,8 +539,8 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
                        uint32_t capacity, uint32_t flags, uint8_t* status) {
   if (!r || (n > 0 && (!bufs || !lens))) return LNX_EINVAL;
   if (capacity > r->cap || (flags & ~(uint32_t)(LNX_TX_CHECKSUM | LNX_TX_FCS)) != 0) return LNX_EINVAL;
-  for (uint64_t i = 0; i < n; ++i)
-    if (lens[i] > capacity || (lens[i] > 0 && !bufs[i])) return LNX_EINVAL;
+  for (uint64_t i = 0; i < n; ++i)  // (with LNX_TX_FCS even an empty frame grows: it needs its buffer)
+    if (lens[i] > capacity || (!bufs[i] && (lens[i] > 0 || (flags & LNX_TX_FCS)))) return LNX_EINVAL;
   if (n == 0) return LNX_OK;
   std::lock_guard<std::mutex> lk(r->mu);
   if (n < r->host_below) {  // below the crossover: no launch
@@ -488,8 +562,10 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
   const uint32_t depth = r->depth, per = r->batch;
   int rc = LNX_OK;
   std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});
+  std::vector<bool> in_place(depth, false);  // the stage's batch was patched in the slots (zero copy)
   // A batch's results reach the caller only from a stream that completed: on
-  // a failed sync its frames, lens and status stay untouched.
+  // a failed sync its lens and status stay untouched (and, when it was
+  // copied, its frames).
   auto drain = [&](uint32_t k) {
     const uint64_t f0 = pending[k].first;
     const uint32_t cnt = pending[k].second;
@@ -497,10 +573,11 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     auto& s = r->st[k];
     const hipError_t se = hipStreamSynchronize(s.s);
     if (se != hipSuccess) return hip_error(se, "tx ring hipStreamSynchronize");
+    const bool copied = !in_place[k];
     parallel_for(cnt, [&](uint32_t a, uint32_t b) {
       for (uint32_t j = a; j < b; ++j) {
         const uint32_t l = s.h_len[j];
-        if (l) std::memcpy(bufs[f0 + j] + offset, s.h_pack + s.h_off[j], l);
+        if (copied && l) std::memcpy(bufs[f0 + j] + offset, s.h_pack + s.h_off[j], l);
         lens[f0 + j] = l;
         if (status) status[f0 + j] = s.h_verdict[j] ? s.h_verdict[j] : s.h_ok[j];
       }
@@ -514,6 +591,27 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     if (rc != LNX_OK) break;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
     auto& s = r->st[sk];
+    // zero copy when the buffers are the ring's slots, in order and within one
+    // 2 GiB window (the transmit kernels' segment mode: non-decreasing starts,
+    // 31-bit offsets from the batch's first byte): the kernels patch them in place
+    bool direct = r->zero_copy;
+    uint64_t base = 0, prev = 0;
+    for (uint32_t j = 0; j < nb && direct; ++j) {
+      uint64_t pos = 0;
+      direct = in_ring(r, bufs[i0 + j], offset, capacity, &pos) && (j == 0 || pos >= prev + capacity) &&
+               pos + capacity - (j ? base : pos) < (1ull << 31) - 64;
+      if (j == 0) base = pos;
+      prev = pos;
+      s.h_off[j] = pos - base;
+      s.h_len[j] = lens[i0 + j];
+    }
+    if (direct) {
+      in_place[sk] = true;
+      rc = enqueue_tx(r, s, nb, 0, capacity, flags, true, base);
+      if (rc == LNX_OK) pending[sk] = {i0, nb}, r->stats.zero_copy_frames += nb;
+      continue;
+    }
+    in_place[sk] = false;
     // each frame's room: the frame, then its padding to 60 bytes and the FCS
     // when they fit `capacity` (else the append leaves it as it is)
     uint64_t o = 0;

@@ -218,6 +218,21 @@ static void TestRunnerPatterns() {
     bad += ok1[k] != wok || v1[k] != wv || got.ok[k] != wok || got.verdict[k] != wv;
   }
   EXPECT(bad == 0, "%d frames differ between the host path, the batched GPU path and the per-frame functions", bad);
+  // RunnerConfig.Buffers carved from the ring (SlotBuffers): one IngressPackets
+  // over the slots the receive handler filled, read in place (zero copy)
+  std::vector<lneto::Bytes> slots = ring.SlotBuffers(), view;
+  for (uint32_t k = 0; k < ring.Slots(); ++k) {
+    std::memcpy(ring.Slot(k), frames[k].data(), frames[k].size());
+    view.emplace_back(slots[k].p, frames[k].size());
+  }
+  std::vector<uint8_t> ok3, v3;
+  EXPECT(ring.IngressPackets(view, 0, ok3, v3) == LNX_OK, "slot-buffer ingress");
+  const lnx_rx_ring_counters c3 = ring.Stats();
+  EXPECT(c3.zero_copy_frames - c2.zero_copy_frames == ring.Slots(), "slot buffers read in place: %llu of %u",
+         (unsigned long long)(c3.zero_copy_frames - c2.zero_copy_frames), ring.Slots());
+  bad = 0;
+  for (uint32_t k = 0; k < ring.Slots(); ++k) bad += ok3[k] != ok1[k] || v3[k] != v1[k];
+  EXPECT(bad == 0, "%d slot-buffer frames differ", bad);
 }
 
 // The receive ring through the C++ mirror: without a GPU it must refuse to

@@ -61,12 +61,14 @@ def test_ring_requires_a_device():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [True, False])
 @pytest.mark.parametrize("offset", [0, 2, 16])
-def test_ring_slots_ingress(cuda, offset):
+def test_ring_slots_ingress(cuda, offset, zero_copy):
     frames = _case_frames(seed=11 + offset, count=1200)
     cap = _cap_for(frames, offset)
     ring = _ring(len(frames) + 7, slot_cap=cap, batch_slots=256, depth=3)
     try:
+        ring.set_zero_copy(zero_copy)
         for i, f in enumerate(frames):
             ring.slots[i + 7, :offset] = 0xEE  # headroom before the frame
             ring.slots[i + 7, offset:offset + len(f)] = np.frombuffer(f, dtype=np.uint8)
@@ -77,6 +79,7 @@ def test_ring_slots_ingress(cuda, offset):
         bad = np.flatnonzero(verdict != want_v)
         assert bad.size == 0, [(int(i), int(verdict[i]), int(want_v[i]), len(frames[i])) for i in bad[:20]]
         assert want_ok.sum() > 900 and (want_ok == 0).sum() > 150
+        assert ring.stats()["zero_copy_frames"] == (len(frames) if zero_copy else 0)
     finally:
         ring.close()
 
@@ -128,12 +131,14 @@ def test_ingress_packets_rejects_oversize(cuda):
 
 
 @pytest.mark.gpu
-def test_ring_mtu_batch_roundtrip(cuda):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_ring_mtu_batch_roundtrip(cuda, zero_copy):
     """64 Ki x 1500-byte frames with FCS through the pipelined ring: all pass;
     then one flipped byte per 1000 frames fails exactly those frames."""
     n, flen = 1 << 16, 1500
     ring = _ring(n, slot_cap=1536, batch_slots=8192, depth=3)
     try:
+        ring.set_zero_copy(zero_copy)
         rng = np.random.default_rng(1)
         data = rng.integers(0, 256, (n, flen - 4), dtype=np.uint8)
         ring.slots[:, : flen - 4] = data
@@ -295,7 +300,8 @@ def test_ring_filter_precedence(cuda, no_fcs):
 
 
 @pytest.mark.gpu
-def test_ring_packed_zipf_lengths(cuda):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_ring_packed_zipf_lengths(cuda, zero_copy):
     """Zipf-mix frames (64-1500 B, mean ~246) in 1536-B slots: the batches are
     packed back to back (PCIe carries the frames, not the slots); every FCS and
     verdict as the oracle says, including corrupted and empty frames."""
@@ -313,6 +319,7 @@ def test_ring_packed_zipf_lengths(cuda):
         frames.append(f)
     ring = _ring(len(frames), slot_cap=1536, batch_slots=1024, depth=3)
     try:
+        ring.set_zero_copy(zero_copy)
         _fill_ring(ring, frames, 0)
         ok, verdict = ring.ingress(0, len(frames))
         ok2, verdict2 = ring.ingress_packets(frames)
@@ -372,3 +379,62 @@ def test_host_threshold_paths_agree(cuda, n):
                 assert bufs[k][:len(fin)].tobytes() == fin, (thr, k)
         finally:
             ring.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offset", [0, 6])
+def test_packets_on_ring_slots(cuda, offset):
+    """Zero copy at the netdev boundary: RunnerConfig.Buffers carved from the
+    ring's slots (x/netdev/runner.go:92-94), so IngressPackets / EgressPackets
+    get views of the ring's pinned memory and the kernels read (egress: patch)
+    the frames in place.  Against the oracle, with the copying path on the same
+    frames, and with the cases that must fall back to staging: a buffer outside
+    the ring, egress buffers out of slot order."""
+    from tests.test_tx_checksum import tx_frames
+    cap = 1536
+    rx = _case_frames(seed=70 + offset, count=700)
+    ring = _ring(1000, slot_cap=cap, batch_slots=256, depth=3)
+    try:
+        views = []
+        for i, f in enumerate(rx):
+            ring.slots[i, :offset] = 0xEE
+            ring.slots[i, offset:offset + len(f)] = np.frombuffer(f, np.uint8)
+            views.append(ring.slots[i, :offset + len(f)])
+        s0 = ring.stats()["zero_copy_frames"]
+        ok, verdict = ring.ingress_packets(views, offset=offset)
+        assert ring.stats()["zero_copy_frames"] - s0 == len(rx)
+        want_ok, want_v = _expect(rx)
+        assert np.array_equal(ok, want_ok) and np.array_equal(verdict, want_v)
+        # one buffer outside the ring: those batches are gathered, same results
+        mixed = list(views)
+        mixed[300] = np.frombuffer(b"\xEE" * offset + rx[300], np.uint8)
+        ok2, verdict2 = ring.ingress_packets(mixed, offset=offset)
+        assert np.array_equal(ok2, want_ok) and np.array_equal(verdict2, want_v)
+
+        # egress in place: frames written by the "stack" into the slots, finished there
+        tx = [f for f in tx_frames(seed=80 + offset, count=900) if len(f) <= cap - offset - 64][:700]
+        capacity = cap - offset
+        for order in ("slots", "reversed"):
+            rng = np.random.default_rng(81)
+            junk = rng.integers(0, 256, (len(tx), cap), dtype=np.uint8)
+            ring.slots[:len(tx)] = junk
+            for i, f in enumerate(tx):
+                ring.slots[i, offset:offset + len(f)] = np.frombuffer(f, np.uint8)
+            idx = list(range(len(tx))) if order == "slots" else list(range(len(tx)))[::-1]
+            bufs = [ring.slots[i] for i in idx]
+            s0 = ring.stats()["zero_copy_frames"]
+            sizes, status = ring.egress_packets(bufs, [len(tx[i]) for i in idx], offset=offset, capacity=capacity)
+            zc = ring.stats()["zero_copy_frames"] - s0
+            assert zc == (len(tx) if order == "slots" else 0), (order, zc)
+            bad = []
+            for k, i in enumerate(idx):
+                want, st = O.tx_checksum(tx[i])
+                want, st2 = O.fcs_append(want, capacity)
+                got = ring.slots[i, offset:offset + int(sizes[k])].tobytes()
+                if got != want or int(status[k]) != (st or st2):
+                    bad.append((order, i, len(tx[i]), int(sizes[k]), len(want), int(status[k])))
+                assert np.array_equal(ring.slots[i, :offset], junk[i, :offset])
+                assert np.array_equal(ring.slots[i, offset + len(want):], junk[i, offset + len(want):]), (order, i)
+            assert not bad, bad[:10]
+    finally:
+        ring.close()
