@@ -756,12 +756,16 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   if (n == 0) return hipSuccess;
   const SlicePlan pl = slice_plan(n, num_cus);
   const uint32_t* img = static_cast<const uint32_t*>(image);
+  // one workgroup per CU even when the batch has fewer slices (small n): the
+  // workgroups past the last slice own nothing and exit after the prologue,
+  // unless the launch has giant slices, whose pieces every workgroup folds
+  const unsigned grid = (unsigned)(pl.grid > (uint64_t)num_cus ? pl.grid : (uint64_t)num_cus);
   if (verify)
-    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3((unsigned)pl.grid), dim3(kStageW * 64), 0, stream,
-                       bytes, off, n, pl.per, img, out, policy, scratch);
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3(grid), dim3(kStageW * 64), 0, stream, bytes, off,
+                       n, pl.per, img, out, policy, scratch);
   else
-    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3((unsigned)pl.grid), dim3(kStageW * 64), 0, stream,
-                       bytes, off, n, pl.per, img, out, policy, scratch);
+    hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3(grid), dim3(kStageW * 64), 0, stream, bytes, off, n,
+                       pl.per, img, out, policy, scratch);
   return hipGetLastError();
 }
 

@@ -346,7 +346,7 @@ def test_host_threshold_paths_agree(cuda, n):
     n = 1, x/netdev/runner.go:432-433)."""
     frames = _case_frames(seed=900 + n, count=n)
     want_ok, want_v = _expect(frames)
-    cap = 1536
+    cap = max(1536, _cap_for(frames, 0) + 64)  # (room for the egress padding and FCS)
     for thr, where in ((L.HOST_BATCH_DEFAULT, "host" if n < L.HOST_BATCH_DEFAULT else "device"), (0, "device")):
         ring = L.RxRing(max(n, 1), slot_cap=cap, batch_slots=128, depth=2, host_threshold=thr)
         try:
