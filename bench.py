@@ -724,7 +724,7 @@ def main():
         elif args.op in ("fcs_verify", "ingress", "tx_checksum"):
             got = d_ok.cpu().numpy()
         elif args.op == "rx_verify":
-            got = d_ok.cpu().numpy() * 256 + d_verdict.cpu().numpy()
+            got = d_ok.cpu().numpy().astype(np.uint32) * 256 + d_verdict.cpu().numpy()
         elif args.op == "search":
             got = d_hit.cpu().numpy()
         elif args.op == "fcs_append":

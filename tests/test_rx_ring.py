@@ -391,8 +391,8 @@ def test_packets_on_ring_slots(cuda, offset):
     frames, and with the cases that must fall back to staging: a buffer outside
     the ring, egress buffers out of slot order."""
     from tests.test_tx_checksum import tx_frames
-    cap = 1536
     rx = _case_frames(seed=70 + offset, count=700)
+    cap = max(1536, _cap_for(rx, offset))
     ring = _ring(1000, slot_cap=cap, batch_slots=256, depth=3)
     try:
         views = []

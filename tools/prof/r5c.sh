@@ -1,6 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -u -m pytest tests/test_rx_ring.py tests/test_abi.py tests/test_rx_verify.py tests/test_stage.py -x -v -s --timeout 300 --timeout-method thread -m gpu > gpurun_out/r5b_stage_tests.log 2>&1 || { echo TESTS_FAILED; exit 1; }
 timeout -k 10 180 python -u bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-slice16m > gpurun_out/r5b_bench_mtu1500.jsonl 2>&1 &&
 timeout -k 10 180 python -u bench.py --steps 50 --warmup 5 --op rx_verify --no-cpu-baseline --verify > gpurun_out/r5b_bench_rx_verify.jsonl 2>&1 &&
 timeout -k 10 180 python -u bench.py --steps 20 --warmup 3 --workload zipf64_1500 --no-cpu-baseline > gpurun_out/r5b_bench_zipf.jsonl 2>&1 &&
