@@ -7,26 +7,22 @@
 // loads.  Two kernels read every frame from HBM twice (0.247 + 0.248 ms on
 // 1 M x 1500 B); this one reads it once.
 //
-// Layout: the ingress kernel's qword rows (ingress_kernel.hip): one 16-lane
-// row per frame, four frames per wave, lane p holding qwords qstart + p + 16u
-// of the frame's 8-byte-aligned base (u < 12 per batch: 1536 bytes per row),
-// the header fields gathered from the row's lanes by ds_bpermute, the sums by
-// v_dot2 on the loaded qwords.  The CRC rides on the same qwords as an
-// interleaved fold: lane p owns the 8-byte chunks p, p + 16, p + 32, ... of a
-// window that starts 16 qwords before qstart (one extra load per lane, the
-// "pre" qword, brings in the frame's first bytes: the MACs the ingress rows
-// never load), and folds one chunk per 128-byte line:
+// The CRC is an interleaved fold over one 16-lane row per frame: lane p owns
+// the 8-byte chunks p, p + 16, p + 32, ... of a qword window that starts at
+// the qword holding the frame's first byte, and folds one chunk per 128-byte
+// line:
 //   r <- Z_128(r ^ w0) ^ Z_124(w1)
 // (eight byte lookups in lane-private slicing tables, the staged kernel's
 // 8-column layout).  After the row's NL lines, lane p's register sits 8p bytes
 // past the window end W; the frame's register is
-//   R = Z_{-b}( XOR_p Z_{-8(p + a)}(r_p) ),  W - Ltot = 8a + b  (b < 8, a <= 16),
+//   R = Z_{-b}( XOR_p Z_{-8(p + a)}(r_p) ),  W - Ltot = 8a + b  (b < 8, a < 16),
 // the first shift by the lane's own nibble tables F_{p+a}, the row XOR by DPP,
 // the last by one of eight nibble tables.  The frame's first four bytes carry
-// the CRC init (XOR 0xFF), bytes before the frame and past its end are masked
-// to zero; FCS ok = Ltot >= 4 and ~R == the CRC-32 residue.
+// the CRC init (XOR 0xFF); FCS ok = Ltot >= 4 and ~R == the CRC-32 residue.
+// The verdicts come from a second phase with one lane per frame (below).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 #include "rx_filter.hpp"
 
 namespace lnx {
@@ -78,6 +74,14 @@ __device__ __forceinline__ uint32_t rv_nib(const char* lds, uint32_t t, uint32_t
   for (uint32_t i = 0; i < 8; ++i) a ^= rv_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
   return a;
 }
+// the same for F_q in its banked layout (entry e of table q at dword 32 e + q)
+__device__ __forceinline__ uint32_t rv_nib_f(const char* lds, uint32_t q, uint32_t v) {
+  uint32_t a = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i)
+    a ^= rv_lds(lds, kRvF + 4u * q + ((16u * i + __builtin_amdgcn_ubfe(v, 4 * i, 4)) << 7));
+  return a;
+}
 __device__ __forceinline__ uint32_t rv_row_xor(uint32_t v) {
   v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
@@ -123,12 +127,38 @@ __device__ __forceinline__ uint32_t rv_dot2(uint32_t w, uint32_t acc) {
 // last `trim` bytes are the FCS (trim 4) or none (LNX_RX_NO_FCS: trim 0, no
 // CRC, ok = 1).  ok[f] = the FCS test, verdict[f] = the verdict of the frame
 // without its FCS, as lnx_ingress_verify_batch_filtered.
+//
+// A wave takes kRvGroup consecutive frames (a group) in two phases:
+//  A. data: kRvGroup / 4 row passes of four frames (one 16-lane row each).
+//     Lane p folds qwords p, p + 16, ... of the frame's qword window into its
+//     CRC register (the first line masked to the frame, the init on its first
+//     four bytes; the later lines unmasked, the last qword's bytes past the
+//     frame taken out again by the lane holding it) and adds every qword into
+//     a raw sum (no per-qword masks: qwords past the frame load as zero); the
+//     lanes holding the FCS / the bytes past the frame take them out, so
+//     S = the LE 16-bit sum of the frame's bytes [14, L).  The row's FCS test,
+//     S and the frame's first kRvHead qwords go to LDS.
+//  B. verdicts: one lane per frame parses the headers from its staged qwords,
+//     takes the header, pseudo-header and head-of-segment sums there, and the
+//     segment's sum as S minus the bytes before it minus the bytes from its
+//     end to L (runt padding, trailing data: staged when short, else summed
+//     from memory by the whole wave).
+// Every qword load reads inside the frame or a zero qword (g_rv_zero), so no
+// load crosses the frame's qwords and none is under a branch; the offsets of
+// a group are loaded once, by the lane of each frame.
+constexpr uint32_t kRvGroup = 48;  // frames per wave and group (LDS: tables + 16 x group staging <= 160 KiB)
+constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 72 - mis) >= [0, 65)
+constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead
+__device__ uint2 g_rv_zero[2];
+
 template <bool CRC, bool FILT>
 __global__ void __launch_bounds__(kRvBlock)
 rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
                  uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
                  const uint32_t* __restrict__ image, RxFilter filt) {
-  __shared__ __attribute__((aligned(16))) char lds[CRC ? kRvBytes : 16];
+  constexpr uint32_t kTabBytes = CRC ? kRvBytes : 0u;
+  constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
+  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
   if constexpr (CRC) {
     const uint32_t t = threadIdx.x;
     for (uint32_t vi = t; vi < 2048u; vi += kRvBlock) {
@@ -138,67 +168,220 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
       row[0] = v4;
       row[1] = v4;
     }
-    for (uint32_t i = t; i < 40u * 128u; i += kRvBlock) reinterpret_cast<uint32_t*>(lds + kRvF)[i] = image[kRvImgF + i];
+    // F_q (q < 32): entry e of table q at dword 32 e + q, so the 16 lanes of a
+    // row (16 different tables) read 16 different banks; B_b as in the image
+    for (uint32_t i = t; i < 32u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
+    for (uint32_t i = t; i < 8u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
     __syncthreads();
   }
   const uint32_t trim = CRC ? 4u : 0u;
-  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
+  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4, wv = threadIdx.x >> 6;
   const RvLane z(lane);
-  const uint64_t nwaves = (uint64_t)gridDim.x * (kRvBlock / 64);
-  for (uint64_t qg = (uint64_t)blockIdx.x * (kRvBlock / 64) + (threadIdx.x >> 6); qg * 4 < n; qg += nwaves) {
-    const uint64_t f = qg * 4 + row;
-    const bool live = f < n;
-    const uint64_t s = live ? off[f] : 0;
-    const uint32_t sl = live && seg_len ? seg_len[f] : 0u;
-    const uint64_t e1 = live && !seg_len ? off[f + 1] : 0;
-    const uint64_t et64 = !live ? 0 : (seg_len ? s + sl : (e1 > s ? e1 : s));
-    const uint64_t lt64 = et64 - s;  // the whole frame, FCS included
-    const uint32_t Lt = lt64 < 0x7FFFFFFFull ? (uint32_t)lt64 : 0x7FFFFFFFu;
+  uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (FCS ok, S) per frame
+  uint2* head = res + kRvGroup;                                                // kRvHead qwords per frame
+  const uint2* zero = g_rv_zero;
+  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
+    // the group's frames: lane k < kRvGroup holds frame g * kRvGroup + k's start and length (FCS included)
+    const uint64_t fk = g * kRvGroup + lane;
+    const bool live = lane < kRvGroup && fk < n;
+    const uint64_t fi = live ? fk : n - 1u;
+    const uint64_t sk = off[fi];
+    const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
+    const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
+    const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
+    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+
+    // ---------------------------------------------------------------- A: data
+    // the row's frame of pass j: its start (from the lane that holds it) and length
+    auto row_frame = [&](uint32_t j, const uint8_t*& fr, uint32_t& Lt) {
+      const uint32_t k = 4u * j + row;
+      const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
+      const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
+      Lt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ltk);
+      fr = bytes + (((uint64_t)shi << 32) | slo);
+    };
+    // the first kRvPf qwords of a pass's batch 0 are loaded during the pass before
+    // (software pipelining: their latency overlaps the previous frame's fold)
+    uint2 pf[kRvPf];
+    const uint8_t* frn;
+    uint32_t Ltn;
+    row_frame(0, frn, Ltn);
+    auto prefetch = [&](const uint8_t* f2, uint32_t L2) {
+      const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(f2) & 7u);
+      const uint2* b2 = reinterpret_cast<const uint2*>(f2 - m2);
+      const int32_t Q2 = (int32_t)((L2 + m2 + 7u) >> 3);
+#pragma unroll
+      for (int u = 0; u < kRvPf; ++u) {
+        const int32_t q = (int32_t)p + 16 * u;
+        pf[u] = *(q < Q2 ? b2 + q : zero);
+      }
+    };
+    prefetch(frn, Ltn);
+    for (uint32_t j = 0; 4u * j < nrow; ++j) {
+      const uint32_t k = 4u * j + row;  // the row's frame in the group
+      const uint8_t* fr = frn;
+      const uint32_t Lt = Ltn;
+      const uint32_t L = Lt > trim ? Lt - trim : 0u;
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
+      const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
+      const int32_t QE = (int32_t)((Lt + mis + 7u) >> 3);  // qwords holding frame bytes
+      const int32_t NL = (QE + 15) >> 4;                   // lines of the window
+      int32_t nit = (QE + 16 * kRvUnroll - 1) / (16 * kRvUnroll), qmin = QE;
+      nit = max(nit, __shfl_xor(nit, 16));
+      nit = max(nit, __shfl_xor(nit, 32));
+      nit = __builtin_amdgcn_readfirstlane(nit);
+      qmin = min(qmin, __shfl_xor(qmin, 16));
+      qmin = min(qmin, __shfl_xor(qmin, 32));
+      qmin = __builtin_amdgcn_readfirstlane(qmin);
+      uint32_t r = 0, S = 0;
+      // one qword: the sum, and the CRC unit (in the window iff `in`)
+      auto fold = [&](uint2 y, int u, int it, bool in) {
+        uint32_t c0 = y.x, c1 = y.y;
+        if (u == 0 && it == 0) {
+          // line 0: the sum from frame offset 14 on; the CRC over the frame's bytes, init on 0..3
+          const int32_t o0 = 8 * (int32_t)p - (int32_t)mis;
+          S = rv_dot2(c0 & rv_keep_from(14 - o0), rv_dot2(c1 & rv_keep_from(10 - o0), S));
+          if constexpr (CRC) {
+            const int32_t ie = (int32_t)(Lt < 4 ? Lt : 4u);
+            c0 = (c0 & rv_range(o0, 0, (int32_t)Lt)) ^ rv_range(o0, 0, ie);
+            c1 = (c1 & rv_range(o0 + 4, 0, (int32_t)Lt)) ^ rv_range(o0 + 4, 0, ie);
+          }
+        } else {
+          S = rv_dot2(c0, rv_dot2(c1, S));
+        }
+        if constexpr (CRC) {
+          const uint32_t nr = rv_unit(lds, r ^ c0, c1, z);
+          r = in ? nr : r;
+        }
+      };
+      {
+        // batch 0: the prefetched qwords, the rest loaded now, then the next pass's prefetch
+        uint2 y[kRvUnroll];
+#pragma unroll
+        for (int u = 0; u < kRvPf; ++u) y[u] = pf[u];
+#pragma unroll
+        for (int u = kRvPf; u < kRvUnroll; ++u) {
+          const int32_t q = (int32_t)p + 16 * u;
+          y[u] = *(q < QE ? base2 + q : zero);
+        }
+        if (4u * (j + 1u) < nrow) {
+          row_frame(j + 1u, frn, Ltn);
+          prefetch(frn, Ltn);
+        }
+        if (p < kRvHead) head[kRvHead * k + p] = y[0];  // the frame's first qwords for phase B
+        if (qmin >= 16 * (kRvUnroll - 1) + 1) {
+          // every row's window covers all twelve lines (MTU frames): no window test
+#pragma unroll
+          for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, 0, true);
+        } else {
+#pragma unroll
+          for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, 0, u < NL);
+        }
+      }
+      for (int32_t it = 1; it < nit; ++it) {
+        uint2 y[kRvUnroll];
+#pragma unroll
+        for (int u = 0; u < kRvUnroll; ++u) {
+          const int32_t q = (int32_t)p + 16 * (u + kRvUnroll * it);
+          y[u] = *(q < QE ? base2 + q : zero);
+        }
+#pragma unroll
+        for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, it, u + kRvUnroll * it < NL);
+      }
+      // the bytes at or past L (the FCS, the last qword's bytes past the frame)
+      // went into S, those past Lt into the CRC of lines >= 1: the lanes that
+      // hold them (qwords qL .. QE - 1, at most two) take them out again
+      const int32_t lastq = QE - 1, qL = (int32_t)((L + mis) >> 3);
+      const int32_t qme = (lastq & 15) == (int32_t)p ? lastq : (qL & 15) == (int32_t)p && qL < lastq ? qL : -1;
+      const uint2 ye = *(qme >= 0 ? base2 + qme : zero);
+      const int32_t oe = 8 * qme - (int32_t)mis;
+      S -= rv_dot2(ye.x & rv_keep_from((int32_t)L - oe), rv_dot2(ye.y & rv_keep_from((int32_t)L - oe - 4), 0u)) &
+           (qme >= 0 && L >= 14 ? ~0u : 0u);
+      uint32_t okf = 1;
+      if constexpr (CRC) {
+        const bool junk = qme == lastq && lastq >= 16;
+        r ^= rv_unit(lds, junk ? ye.x & rv_keep_from((int32_t)Lt - oe) : 0u,
+                     junk ? ye.y & rv_keep_from((int32_t)Lt - oe - 4) : 0u, z);
+        // the window ends W = 128 NL - mis (frame offsets) past the frame start; W - Lt = 8a + b
+        const uint32_t pad = (uint32_t)(128 * NL - (int32_t)mis - (int32_t)Lt);
+        const uint32_t a = pad >> 3, b = pad & 7u;
+        const uint32_t x = rv_row_xor(rv_nib_f(lds, p + a, r));
+        const uint32_t R = rv_nib(lds, kRvB + 512u * b, x);
+        okf = Lt >= 4 && ~R == 0x2144DF1Cu;
+      }
+      S = rv_row_add(S);
+      if (p == 0) res[k] = make_uint2(okf, S);
+    }
+    __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, read back in order below)
+
+    // ---------------------------------------------------------------- B: verdicts
+    const uint64_t f = fk;
+    const uint32_t Lt = Ltk;
     const uint32_t L = Lt > trim ? Lt - trim : 0u;  // the frame the verdict sees
-    const uint8_t* fr = bytes + s;
+    const uint8_t* fr = bytes + sk;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
-    // qword Q of base2 holds frame offsets 8Q - mis .. 8Q - mis + 7
-    const int32_t qstart = (int32_t)((12 + mis) >> 3);        // qword holding frame offset 12
-    const int32_t QE = (int32_t)((Lt + mis + 7) >> 3);         // qwords touching the frame, FCS included
-    const int32_t kstart = (int32_t)((12 + mis) >> 2);         // dword holding frame offset 12
-
-    // ---- first batch (qwords qstart + p + 16 u) and the pre qword (qstart + p - 16)
-    uint2 y[kRvUnroll];
+    const int32_t QE = (int32_t)((Lt + mis + 7u) >> 3);
+    const uint32_t kk = lane < kRvGroup ? lane : 0u;
+    // the staged qwords 0 .. kRvHead - 1 of the frame's window (frame offsets -mis .. 72 - mis),
+    // then qwords 9, 10 from memory for the frames that need them (IPv4 options past offset 64)
+    uint32_t dw[22];
 #pragma unroll
-    for (int u = 0; u < kRvUnroll; ++u) {
-      const int32_t q = qstart + (int32_t)p + 16 * u;
-      y[u] = q < QE ? base2[q] : make_uint2(0u, 0u);
+    for (uint32_t i = 0; i < kRvHead; ++i) {
+      const uint2 v = head[kRvHead * kk + i];
+      dw[2 * i] = v.x;
+      dw[2 * i + 1] = v.y;
     }
-    const int32_t qpre = qstart + (int32_t)p - 16;
-    uint2 yp = make_uint2(0u, 0u);
-    if constexpr (CRC) yp = qpre >= 0 && qpre < QE ? base2[qpre] : make_uint2(0u, 0u);
-
-    // dword kstart + kk of this row (kk < 31) from the lane that loaded it
-    auto rowword = [&](int32_t kk) -> uint32_t {
-      const uint32_t rel = (uint32_t)(kstart - 2 * qstart + kk);
-      const int addr = (int)((row * 16u + ((rel >> 1) & 15u)) * 4u);
-      const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)y[0].x);
-      const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)y[0].y);
-      return (rel & 1u) ? b : a;
-    };
-    const uint32_t sh = (12 + mis) & 3u;
-    const uint32_t w0 = rowword(0), w1 = rowword(1), w2 = rowword(2), w3 = rowword(3);
-    const uint32_t H0 = __builtin_amdgcn_alignbyte(w1, w0, sh);  // frame bytes 12..15
-    const uint32_t H1 = __builtin_amdgcn_alignbyte(w2, w1, sh);  // 16..19
-    const uint32_t H2 = __builtin_amdgcn_alignbyte(w3, w2, sh);  // 20..23
+    // the frame's bytes 4k .. 4k + 3 as one dword, k < 15 (offsets < 60)
+    const uint32_t sh = mis & 3u;
+    uint32_t F[15];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const uint32_t lo = mis >= 4 ? dw[k + 1] : dw[k], hi = mis >= 4 ? dw[k + 2] : dw[k + 1];
+      F[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
     auto byt = [](uint32_t w, int i) -> uint32_t { return (w >> (8 * i)) & 0xFFu; };
-    auto be = [&](uint32_t w, int i) -> uint32_t { return (byt(w, i) << 8) | byt(w, i + 1); };
-    auto field16 = [&](uint32_t o) -> uint32_t {
-      const int32_t kk = (int32_t)((o + mis) >> 2) - kstart;
-      const uint32_t lo = rowword(kk), hi = rowword(kk + 1);
-      const uint32_t v2 = __builtin_amdgcn_alignbyte(hi, lo, (o + mis) & 3u);
-      return ((v2 & 0xFFu) << 8) | ((v2 >> 8) & 0xFFu);
+    auto be16 = [&](int o) -> uint32_t {  // the big-endian 16-bit field at static frame offset o (o < 59)
+      const uint32_t w = (o & 3) == 3 ? __builtin_amdgcn_alignbyte(F[(o >> 2) + 1], F[o >> 2], 3) : F[o >> 2];
+      const int i = (o & 3) == 3 ? 0 : (o & 3);
+      return (byt(w, i) << 8) | byt(w, i + 1);
     };
-    auto field32 = [&](uint32_t o) -> uint32_t {
-      const int32_t kk = (int32_t)((o + mis) >> 2) - kstart;
-      return __builtin_amdgcn_alignbyte(rowword(kk + 1), rowword(kk), (o + mis) & 3u);
+    auto le32 = [&](int o) -> uint32_t {  // the frame's bytes o .. o + 3 (o % 4 == 2 or 0)
+      return (o & 3) == 0 ? F[o >> 2] : __builtin_amdgcn_alignbyte(F[(o >> 2) + 1], F[o >> 2], (uint32_t)(o & 3));
     };
+    // a field at a header-length-dependent offset o (o + 2 <= L checked by the caller): staged, else from memory
+    auto dyn16 = [&](uint32_t o) -> uint32_t {
+      const uint32_t a = o + mis;  // byte of the window
+      uint32_t b0, b1;
+      if (a + 2u <= 8u * kRvHead) {
+        const uint8_t* hb = reinterpret_cast<const uint8_t*>(head + kRvHead * kk);
+        b0 = hb[a];
+        b1 = hb[a + 1u];
+      } else {
+        b0 = fr[o];
+        b1 = fr[o + 1u];
+      }
+      return (b0 << 8) | b1;
+    };
+    // LE 16-bit sum of the frame's bytes [a, b) among dwords D0 .. D1 - 1 of dw
+    // (those that can hold them: frame offset o lies in dword (o + mis) / 4, mis < 8)
+    auto hsum = [&](auto D0, auto D1, int32_t a, int32_t b) -> uint32_t {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int d = decltype(D0)::value; d < decltype(D1)::value; ++d)
+        acc = rv_dot2(dw[d] & rv_range(4 * d - (int32_t)mis, a, b), acc);
+      return acc;
+    };
+    using I3 = std::integral_constant<int, 3>;
+    using I5 = std::integral_constant<int, 5>;
+    using I8 = std::integral_constant<int, 8>;
+    using I11 = std::integral_constant<int, 11>;
+    using I16 = std::integral_constant<int, 16>;
+    using I18 = std::integral_constant<int, 18>;
+    using I22 = std::integral_constant<int, 22>;
 
     // ---- header parse (ingress_kernel.hip's, FCS excluded: L bytes)
     uint32_t v = 0, v_udp4 = 0;
@@ -208,14 +391,11 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     if (L < 14) {
       v = kErrTruncatedFrame;
     } else {
-      const uint32_t et = be(H0, 0);
+      const uint32_t et = be16(12);
       bool eth_drop = false, et_handler = true;
       if (FILT && filt.on) {
-        // StackEthernet.Demux (internet/stack-ethernet.go:146-152), before ValidateSize; the
-        // destination MAC (frame bytes 0..5) from the pre qwords and the first batch
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(fr - mis) + (mis >> 2);
-        const uint32_t sm = mis & 3u, m0 = w[0], m1 = w[1], m2 = w[2];
-        const uint32_t D0 = __builtin_amdgcn_alignbyte(m1, m0, sm), D1 = __builtin_amdgcn_alignbyte(m2, m1, sm) & 0xFFFFu;
+        // StackEthernet.Demux (internet/stack-ethernet.go:146-152), before ValidateSize
+        const uint32_t D0 = F[0], D1 = F[1] & 0xFFFFu;
         const bool bcast = D0 == 0xFFFFFFFFu && D1 == 0xFFFFu;
         const bool mine = D0 == filt.mac_lo && D1 == filt.mac_hi;
         eth_drop = !bcast && !mine && !(filt.eth_mc && (D0 & 1u));
@@ -236,9 +416,9 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
         if (M < 20) {
           v = kErrTruncatedFrame;
         } else {
-          const uint32_t b0 = byt(H0, 2), tl = be(H1, 0), ihl = b0 & 15u;
+          const uint32_t b0 = byt(F[3], 2), tl = be16(16), ihl = b0 & 15u;
           if (FILT && filt.on && filt.ip4 != 0u) {
-            const uint32_t dst = field32(30);  // demux4's destination check (stack-ip4.go:108-119)
+            const uint32_t dst = le32(30);  // demux4's destination check (stack-ip4.go:108-119)
             const bool mc = (dst & 0xF0u) == 0xE0u, bc = dst == 0xFFFFFFFFu;
             if (dst != filt.ip4 && !(filt.ip4_mc && mc) && !(filt.ip4_bc && bc)) v = kErrPacketDrop;
           }
@@ -247,10 +427,10 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
           else if (tl > M) v = kErrTruncatedFrame;
           else if (ihl < 5 || ihl * 4 > tl) v = kErrInvalidLengthField;
           else if ((b0 >> 4) != 4) v = kErrInvalidField;
-          else if ((flags & kVerifyEvilBit) && (be(H2, 0) & (1u << 13))) v = kErrPacketDrop;
+          else if ((flags & kVerifyEvilBit) && (be16(20) & (1u << 13))) v = kErrPacketDrop;
           if (v == 0) {
             hdr_sum = true;
-            const uint32_t hl = ihl * 4, proto = byt(H2, 3), P = tl - hl;
+            const uint32_t hl = ihl * 4, proto = byt(F[5], 3), P = tl - hl;
             if (FILT && filt.on && !rv_proto_bit(filt.p4, proto)) {
               v_udp4 = kErrPacketDrop;  // nodeByProto nil (stack-ip4.go:135-141), after the header sum
             } else if (proto == 6) {
@@ -261,7 +441,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
               if (P < 8) {
                 v_udp4 = kErrTruncatedFrame;
               } else {
-                const uint32_t ul = field16(14 + hl + 4);
+                const uint32_t ul = dyn16(14 + hl + 4);
                 if (ul < 8) v_udp4 = kErrInvalidLengthField;
                 else if (ul > P) v_udp4 = kErrTruncatedFrame;
                 else {
@@ -274,7 +454,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
               if (P < 8) {
                 v_udp4 = kErrTruncatedFrame;
               } else {
-                const uint32_t type = field16(14 + hl) >> 8;
+                const uint32_t type = dyn16(14 + hl) >> 8;
                 if (type != 0 && type != 8) {
                   v_udp4 = kErrPacketDrop;
                 } else {
@@ -290,9 +470,9 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
         if (M < 40) {
           v = kErrTruncatedFrame;
         } else {
-          const uint32_t pl = be(H1, 2), proto = byt(H2, 0);
+          const uint32_t pl = be16(18), proto = byt(F[5], 0);
           if (FILT && filt.on && (filt.ip6[0] | filt.ip6[1] | filt.ip6[2] | filt.ip6[3]) != 0u) {
-            const uint32_t d0 = field32(38), d1 = field32(42), d2 = field32(46), d3 = field32(50);
+            const uint32_t d0 = le32(38), d1 = le32(42), d2 = le32(46), d3 = le32(50);
             const bool mine = d0 == filt.ip6[0] && d1 == filt.ip6[1] && d2 == filt.ip6[2] && d3 == filt.ip6[3];
             if (!mine && !(filt.ip6_mc && (d0 & 0xFFu) == 0xFFu)) v = kErrPacketDrop;
           }
@@ -305,8 +485,8 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
             if (proto == 58 && pl < 8) v = kErrTruncatedFrame;
             if (proto == 17) {
               if (pl < 8) v = kErrTruncatedFrame;
-              else if (field16(58) < 8) v = kErrInvalidLengthField;
-              else if (field16(58) > pl) v = kErrTruncatedFrame;
+              else if (be16(58) < 8) v = kErrInvalidLengthField;
+              else if (be16(58) > pl) v = kErrTruncatedFrame;
             }
             if (v == 0) {
               l4_sum = true;
@@ -318,81 +498,48 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
       }
     }
 
-    // ---- one pass over the frame's qwords: the sums (qwords below qend) and the CRC (every qword)
-    const bool any_sum = hdr_sum || l4_sum;
-    const int32_t end = l4_sum ? lb : (hdr_sum ? 34 : 0);
-    const int32_t kend = any_sum ? (end + (int32_t)mis + 3) >> 2 : 0;
-    const int32_t qend = (kend + 1) >> 1;
-    const int32_t ha = hdr_sum ? 14 : 0, hb = hdr_sum ? 34 : 0;
-    uint32_t hS = 0, tS = 0;
-    // CRC: lines (16 qwords) from qword qstart - 16; the row needs NL of them
-    const int32_t q0 = qstart - 16;
-    const int32_t NL = (QE - q0 + 15) >> 4;  // >= 1
-    const int32_t lastq = QE - 1;
-    // the last qword's bytes at or past Lt are not the frame's
-    const int32_t olast = 8 * lastq - (int32_t)mis;
-    const uint32_t mlast0 = ~rv_keep_from((int32_t)Lt - olast), mlast1 = ~rv_keep_from((int32_t)Lt - olast - 4);
-    uint32_t r = 0;
-    if constexpr (CRC) {
-      // the pre qword (line 0): bytes before the frame masked, the CRC init on frame bytes 0..3
-      const int32_t o0 = 8 * qpre - (int32_t)mis;
-      const int32_t ie = (int32_t)(Lt < 4 ? Lt : 4u);
-      const uint32_t a0 = yp.x & rv_range(o0, 0, (int32_t)Lt), a1 = yp.y & rv_range(o0 + 4, 0, (int32_t)Lt);
-      const uint32_t x0 = a0 ^ rv_range(o0, 0, ie), x1 = a1 ^ rv_range(o0 + 4, 0, ie);
-      r = rv_unit(lds, x0, x1, z);  // (NL >= 1: line 0 is always the row's)
-    }
-    // a wave-uniform trip count (the most any row of the wave needs), as the ingress kernel
-    const int32_t qneed = QE > qend ? QE : qend;
-    int32_t nit = qneed > qstart ? (qneed - qstart + 16 * kRvUnroll - 1) / (16 * kRvUnroll) : 0;
-    nit = max(nit, __shfl_xor(nit, 16));
-    nit = max(nit, __shfl_xor(nit, 32));
-    nit = __builtin_amdgcn_readfirstlane(nit);
-    uint2 yl = make_uint2(0u, 0u);  // the sum's last qword, on the lane that holds it
-    for (int32_t it = 0; it < nit; ++it) {
-      const int32_t qb = qstart + (int32_t)p + 16 * kRvUnroll * it;
-      if (it > 0) {
+    // ---- the sums: header [14, 34) and pseudo-header [pa, pb) from the staged
+    // bytes; the segment [la, lb) = S - [14, la) - [lb, L)
+    // (IPv4 options past the staged bytes: qwords 9 and 10 from memory)
 #pragma unroll
-        for (int u = 0; u < kRvUnroll; ++u) {
-          const int32_t q = qb + 16 * u;
-          y[u] = q < QE ? base2[q] : make_uint2(0u, 0u);
-        }
+    for (int i = 0; i < 2; ++i) {
+      const int32_t q = (int32_t)kRvHead + i;
+      const bool need = l4_sum && la + (int32_t)mis > 8 * (int32_t)kRvHead && q < QE;
+      const uint2 v2 = *(need ? base2 + q : zero);
+      dw[2 * q] = v2.x;
+      dw[2 * q + 1] = v2.y;
+    }
+    const uint32_t hS = hdr_sum ? hsum(I3{}, I11{}, 14, 34) : 0u;  // bytes 14..33: dwords 3..10
+    // the bytes from the segment's end to L: staged when they end inside the
+    // staged qwords, else the whole wave sums them from memory (one frame at a time)
+    const bool tail = l4_sum && lb < (int32_t)L;
+    const bool tail_staged = tail && (int32_t)(L + mis) <= 8 * (int32_t)kRvHead;
+    uint32_t tS = tail_staged ? hsum(I8{}, I18{}, lb, (int32_t)L) : 0u;  // lb >= 34, L + mis <= 72
+    uint64_t longt = __builtin_amdgcn_ballot_w64(tail && !tail_staged);
+    while (longt) {
+      const uint32_t kf = (uint32_t)__builtin_ctzll(longt);
+      longt &= longt - 1u;
+      const int32_t a = __builtin_amdgcn_readlane(lb, kf), b = __builtin_amdgcn_readlane((int32_t)L, kf);
+      const uint64_t s2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, kf)) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), kf) << 32);
+      const uint8_t* fr2 = bytes + s2;
+      const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(fr2) & 7u);
+      const uint2* kb = reinterpret_cast<const uint2*>(fr2 - m2);
+      const int32_t q0 = (a + (int32_t)m2) >> 3, q1 = (b + (int32_t)m2 + 7) >> 3;
+      uint32_t acc = 0;
+      for (int32_t qb = q0; qb < q1; qb += 64) {  // (a wave-uniform trip count)
+        const int32_t q = qb + (int32_t)lane;
+        const uint2 t = *(q < q1 ? kb + q : zero);
+        const int32_t o0 = 8 * q - (int32_t)m2;
+        acc = rv_dot2(t.x & rv_range(o0, a, b), rv_dot2(t.y & rv_range(o0 + 4, a, b), acc));
       }
 #pragma unroll
-      for (int u = 0; u < kRvUnroll; ++u) {
-        const int32_t q = qb + 16 * u;
-        // sums: qwords below qend only; the first qword of the first batch takes the header /
-        // pseudo-header / transport-start masks (every later one lies past offset 126)
-        const bool insum = q < qend;
-        const uint32_t sx = insum ? y[u].x : 0u, sy = insum ? y[u].y : 0u;
-        if (u == 0 && it == 0) {
-          const int32_t o0 = 8 * q - (int32_t)mis;
-          hS = rv_dot2(sx & rv_range(o0, ha, hb), hS);
-          hS = rv_dot2(sy & rv_range(o0 + 4, ha, hb), hS);
-          tS = rv_dot2(sx & (rv_range(o0, pa, pb) | rv_range(o0, la, lb)), tS);
-          tS = rv_dot2(sy & (rv_range(o0 + 4, pa, pb) | rv_range(o0 + 4, la, lb)), tS);
-        } else {
-          tS = rv_dot2(sx, rv_dot2(sy, tS));
-          const bool isl = q == qend - 1;
-          yl.x = isl ? y[u].x : yl.x;
-          yl.y = isl ? y[u].y : yl.y;
-        }
-        if constexpr (CRC) {
-          // line 1 + u + kRvUnroll * it of the CRC window
-          const bool inl = 1 + u + kRvUnroll * it < NL;
-          const bool isl = q == lastq;
-          const uint32_t c0 = isl ? y[u].x & mlast0 : y[u].x, c1 = isl ? y[u].y & mlast1 : y[u].y;
-          const uint32_t nr = rv_unit(lds, r ^ c0, c1, z);
-          r = inl ? nr : r;
-        }
-      }
+      for (int sft = 1; sft < 64; sft <<= 1) acc += (uint32_t)__shfl_xor((int)acc, sft);
+      tS += lane == kf ? acc : 0u;
     }
-    // bytes at or past lb of the sum's last qword (zero unless this lane kept it)
-    {
-      const int32_t ol = 8 * (qend - 1) - (int32_t)mis;
-      const uint32_t j0 = yl.x & rv_keep_from(lb - ol), j1 = yl.y & rv_keep_from(lb - ol - 4);
-      tS -= rv_dot2(j0, rv_dot2(j1, 0u));
-    }
-    hS = rv_row_add(hS), tS = rv_row_add(tS);
+    const uint2 rk = res[kk];
+    // [14, la): la <= 74; [pa, pb) within [22, 54)
+    if (l4_sum) tS = rk.y - hsum(I3{}, I22{}, 14, la) - tS + hsum(I5{}, I16{}, pa, pb);
     auto conv = [&](uint32_t S) -> uint32_t {  // ingress_kernel.hip: the byte rotation for even bases
       if (mis & 1u) return S;
       uint32_t fo = (S & 0xFFFFu) + (S >> 16);
@@ -403,19 +550,11 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     if (v == 0 && hdr_sum && rv_sum16(hX) != 0) v = kErrBadCRC;
     if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
     if (v == 0 && l4_sum && rv_sum16(tX + lseed) != 0) v = kErrBadCRC;
-    uint32_t okf = 1;
-    if constexpr (CRC) {
-      // the window end W = 8 (q0 + 16 NL) - mis (frame offset); W - Lt = 8a + b
-      const uint32_t pad = (uint32_t)(8 * (q0 + 16 * NL) - (int32_t)mis - (int32_t)Lt);
-      const uint32_t a = pad >> 3, b = pad & 7u;
-      const uint32_t x = rv_row_xor(rv_nib(lds, kRvF + 512u * (p + a), r));
-      const uint32_t R = rv_nib(lds, kRvB + 512u * b, x);
-      okf = Lt >= 4 && ~R == 0x2144DF1Cu;
-    }
-    if (live && p == 0) {
-      okv[f] = (uint8_t)okf;
+    if (live) {
+      okv[f] = (uint8_t)rk.x;
       verdict[f] = (uint8_t)v;
     }
+    __builtin_amdgcn_wave_barrier();  // the next group rewrites res and head
   }
 }
 
@@ -425,7 +564,7 @@ hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t 
   RxFilter filt{};
   if (filter) filt = *filter;
   if (n == 0) return hipSuccess;
-  uint64_t grid = (n + (kRvBlock / 64) * 4 - 1) / ((kRvBlock / 64) * 4);
+  uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
 #define LNX_RV(C, F)                                                                                       \
   hipLaunchKernelGGL((rx_verify_kernel<C, F>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, off, n, \

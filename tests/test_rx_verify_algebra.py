@@ -1,11 +1,13 @@
 """The CRC algebra of the fused receive kernel (lneto_amd/csrc/rx_verify_kernel.hip,
 DESIGN.md §3.12) restated on the host and checked against zlib (the arithmetic of
 ethernet.CRC32, lneto ethernet/crc.go:19-21): 16 lanes fold the interleaved
-8-byte chunks of a window that starts 16 qwords before the qword holding frame
-offset 12, r <- Z_128(r ^ w0) ^ Z_124(w1) per 128-byte line, the frame's
-first bytes carrying the init, the bytes around the frame masked; then
-R = Z_{-b}(XOR_p Z_{-8(p + a)}(r_p)).  Every length 0..300 and long frames, at
-every base alignment mod 8, with garbage before and after the frame."""
+8-byte chunks of a window that starts at the qword holding the frame's first
+byte, r <- Z_128(r ^ w0) ^ Z_124(w1) per 128-byte line; the first line masked
+to the frame with the init on its first four bytes, the later lines unmasked
+(the last qword's bytes past the frame removed again by the lane that holds
+it); then R = Z_{-b}(XOR_p Z_{-8(p + a)}(r_p)).  Every length 0..300 and long
+frames, at every base alignment mod 8, with garbage before and after the
+frame."""
 import zlib
 
 import numpy as np
@@ -62,40 +64,36 @@ def _range(o0, a, b):
 
 def _fused_crc_register(buf: bytes, mis: int, Lt: int) -> int:
     """The kernel's register after the frame buf[mis : mis + Lt] (buf 8-aligned at index 0)."""
-    le = lambda q, h: int.from_bytes(buf[8 * q + 4 * h: 8 * q + 4 * h + 4], "little") if 0 <= q < QE else 0
-    qstart = (12 + mis) >> 3
     QE = (Lt + mis + 7) >> 3
-    q0 = qstart - 16
-    NL = (QE - q0 + 15) >> 4
+    le = lambda q, h: int.from_bytes(buf[8 * q + 4 * h: 8 * q + 4 * h + 4], "little") if 0 <= q < QE else 0
+    NL = (QE + 15) >> 4
     lastq = QE - 1
-    olast = 8 * lastq - mis
+    ie = min(Lt, 4)
     keep = lambda k: (0xFFFFFFFF << (8 * min(max(k, 0), 4))) & 0xFFFFFFFF
-    mlast0, mlast1 = ~keep(Lt - olast) & 0xFFFFFFFF, ~keep(Lt - olast - 4) & 0xFFFFFFFF
     regs = []
     for p in range(16):
-        # line 0: the pre qword
-        q = qstart + p - 16
-        o0 = 8 * q - mis
-        ie = min(Lt, 4)
-        x0 = (le(q, 0) & _range(o0, 0, Lt)) ^ _range(o0, 0, ie)
-        x1 = (le(q, 1) & _range(o0 + 4, 0, Lt)) ^ _range(o0 + 4, 0, ie)
-        r = _unit(x0, x1)
-        for line in range(1, NL):
-            q = qstart + p + 16 * (line - 1)
+        r = 0
+        for line in range(NL):
+            q = p + 16 * line
             c0, c1 = le(q, 0), le(q, 1)
-            if q == lastq:
-                c0, c1 = c0 & mlast0, c1 & mlast1
+            if line == 0:  # unit 0: the frame's bytes only, the CRC init on its first four
+                o0 = 8 * q - mis
+                c0 = (c0 & _range(o0, 0, Lt)) ^ _range(o0, 0, ie)
+                c1 = (c1 & _range(o0 + 4, 0, Lt)) ^ _range(o0 + 4, 0, ie)
             r = _unit(r ^ c0, c1)
+        # the last qword's bytes past the frame went in unmasked (lines >= 1): the
+        # lane that holds it takes their part out again (it was that lane's last unit)
+        if lastq >= 16 and (lastq & 15) == p:
+            ol = 8 * lastq - mis
+            r ^= _unit(le(lastq, 0) & keep(Lt - ol), le(lastq, 1) & keep(Lt - ol - 4))
         regs.append(r)
-    pad = 8 * (q0 + 16 * NL) - mis - Lt
+    pad = 128 * NL - mis - Lt
     a, b = pad >> 3, pad & 7
     assert 0 <= a < 16
     x = 0
     for p in range(16):
         x ^= _nib(F[p + a], regs[p])
     return _nib(B[b], x)
-
-
 
 
 def test_fused_crc_algebra_all_lengths_and_alignments():

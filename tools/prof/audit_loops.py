@@ -49,8 +49,9 @@ def kernels(lines):
     for i, l in enumerate(lines):
         m = re.match(r"^(_Z\w+):", l)
         if m:
-            j = next(k for k in range(i, len(lines)) if lines[k].strip().startswith("s_endpgm"))
-            out.append((m.group(1), i, j))
+            j = next((k for k in range(i, len(lines)) if lines[k].strip().startswith("s_endpgm")), None)
+            if j is not None:  # (a data symbol, e.g. a __device__ variable, has no code)
+                out.append((m.group(1), i, j))
     return out
 
 

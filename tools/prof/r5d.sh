@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+bash tools/prof/profile.sh r5d mtu1500 rx_verify &&
+bash tools/prof/profile.sh r5d mtu1500 &&
+bash tools/prof/profile.sh r5d zipf64_1500
