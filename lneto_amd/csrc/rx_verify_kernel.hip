@@ -41,6 +41,17 @@ constexpr uint32_t kRvT = 0, kRvF = 65536, kRvB = kRvF + 32 * 512, kRvBytes = kR
 // the compact image (api.cpp build_rx_image): T_k[e] at 256 k + e, then F, then B (dwords)
 constexpr uint32_t kRvImgF = 2048;  // (then B at kRvImgF + 32 * 128; 2048 + 40 * 128 dwords in all)
 
+// A qword load through the global address space: the pointer is a select of
+// a frame address and g_rv_zero, which hipcc would otherwise load with a FLAT
+// instruction -- counted in lgkmcnt too, so every LDS wait of the fold would
+// wait for the frame loads in flight (the prefetch included).
+__device__ __forceinline__ uint2 rv_ld(const uint2* p) {
+  const uint64_t v = *(const __attribute__((address_space(1))) uint64_t*)p;
+  return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+__device__ __forceinline__ uint32_t rv_ld32(const uint32_t* p) {
+  return *(const __attribute__((address_space(1))) uint32_t*)p;
+}
 __device__ __forceinline__ uint32_t rv_lds(const char* lds, uint32_t a) {
   return *reinterpret_cast<const uint32_t*>(lds + a);
 }
@@ -216,7 +227,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
 #pragma unroll
       for (int u = 0; u < kRvPf; ++u) {
         const int32_t q = (int32_t)p + 16 * u;
-        pf[u] = *(q < Q2 ? b2 + q : zero);
+        pf[u] = rv_ld(q < Q2 ? b2 + q : zero);
       }
     };
     prefetch(frn, Ltn);
@@ -265,7 +276,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
 #pragma unroll
         for (int u = kRvPf; u < kRvUnroll; ++u) {
           const int32_t q = (int32_t)p + 16 * u;
-          y[u] = *(q < QE ? base2 + q : zero);
+          y[u] = rv_ld(q < QE ? base2 + q : zero);
         }
         if (4u * (j + 1u) < nrow) {
           row_frame(j + 1u, frn, Ltn);
@@ -286,7 +297,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
 #pragma unroll
         for (int u = 0; u < kRvUnroll; ++u) {
           const int32_t q = (int32_t)p + 16 * (u + kRvUnroll * it);
-          y[u] = *(q < QE ? base2 + q : zero);
+          y[u] = rv_ld(q < QE ? base2 + q : zero);
         }
 #pragma unroll
         for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, it, u + kRvUnroll * it < NL);
@@ -296,7 +307,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
       // hold them (qwords qL .. QE - 1, at most two) take them out again
       const int32_t lastq = QE - 1, qL = (int32_t)((L + mis) >> 3);
       const int32_t qme = (lastq & 15) == (int32_t)p ? lastq : (qL & 15) == (int32_t)p && qL < lastq ? qL : -1;
-      const uint2 ye = *(qme >= 0 ? base2 + qme : zero);
+      const uint2 ye = rv_ld(qme >= 0 ? base2 + qme : zero);
       const int32_t oe = 8 * qme - (int32_t)mis;
       S -= rv_dot2(ye.x & rv_keep_from((int32_t)L - oe), rv_dot2(ye.y & rv_keep_from((int32_t)L - oe - 4), 0u)) &
            (qme >= 0 && L >= 14 ? ~0u : 0u);
@@ -361,8 +372,11 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
         b0 = hb[a];
         b1 = hb[a + 1u];
       } else {
-        b0 = fr[o];
-        b1 = fr[o + 1u];
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(base2) + (a >> 2);
+        const uint32_t lo = rv_ld32(w), hi = (a & 3u) == 3u ? rv_ld32(w + 1) : 0u;
+        const uint32_t v2 = __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
+        b0 = v2 & 0xFFu;
+        b1 = (v2 >> 8) & 0xFFu;
       }
       return (b0 << 8) | b1;
     };
@@ -505,7 +519,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     for (int i = 0; i < 2; ++i) {
       const int32_t q = (int32_t)kRvHead + i;
       const bool need = l4_sum && la + (int32_t)mis > 8 * (int32_t)kRvHead && q < QE;
-      const uint2 v2 = *(need ? base2 + q : zero);
+      const uint2 v2 = rv_ld(need ? base2 + q : zero);
       dw[2 * q] = v2.x;
       dw[2 * q + 1] = v2.y;
     }
@@ -529,7 +543,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
       uint32_t acc = 0;
       for (int32_t qb = q0; qb < q1; qb += 64) {  // (a wave-uniform trip count)
         const int32_t q = qb + (int32_t)lane;
-        const uint2 t = *(q < q1 ? kb + q : zero);
+        const uint2 t = rv_ld(q < q1 ? kb + q : zero);
         const int32_t o0 = 8 * q - (int32_t)m2;
         acc = rv_dot2(t.x & rv_range(o0, a, b), rv_dot2(t.y & rv_range(o0 + 4, a, b), acc));
       }
