@@ -328,8 +328,9 @@ int lnx_rx_ring_stats(lnx_rx_ring* ring, lnx_rx_ring_counters* out);
  * lnx_rx_ring_ingress and, when every buffer of a batch lies in the ring's slot
  * memory (netdev RunnerConfig.Buffers carved from lnx_rx_ring_slots,
  * x/netdev/runner.go:92-94), lnx_ingress_packets and lnx_egress_packets (whose
- * kernels then patch the frames in place: egress also needs the buffers in
- * slot order).  Other buffers are gathered into pinned staging as before.
+ * kernel then patches the frames in place: one read of each frame, stores of
+ * the fields, padding and FCS only).  Other buffers are gathered into pinned
+ * staging as before.
  * on = 0 selects the copying forms for every batch. */
 int lnx_rx_ring_set_zero_copy(lnx_rx_ring* ring, int on);
 

@@ -160,7 +160,7 @@ std::vector<uint32_t> build_stage_image() {
 // T_k[e] = Z_128(e << 8k), T_{4+k}[e] = Z_124(e << 8k) (k < 4), then the nibble
 // tables of Z_{-8q} (q < 32) and Z_{-b} (b < 8), entry (t, i, v) at 128 t + 16 i + v.
 std::vector<uint32_t> build_rx_image() {
-  std::vector<uint32_t> t(2048 + 40 * 128);
+  std::vector<uint32_t> t(2048 + 56 * 128);
   for (uint32_t k = 0; k < 4; ++k)
     for (uint32_t e = 0; e < 256; ++e) {
       t[256 * k + e] = zshift_bytes(e << (8 * k), 128);
@@ -170,6 +170,10 @@ std::vector<uint32_t> build_rx_image() {
     for (uint32_t i = 0; i < 8; ++i)
       for (uint32_t v = 0; v < 16; ++v)
         t[2048 + 128 * q + 16 * i + v] = zshift_bytes(v << (4 * i), q < 32 ? -8 * (int64_t)q : -(int64_t)(q - 32));
+  // then Z_{2^m}, m < 16: the transmit kernel's CRC corrections for the fields it writes
+  for (uint32_t m = 0; m < 16; ++m)
+    for (uint32_t i = 0; i < 8; ++i)
+      for (uint32_t v = 0; v < 16; ++v) t[2048 + 40 * 128 + 128 * m + 16 * i + v] = zshift_bytes(v << (4 * i), 1ll << m);
   return t;
 }
 

@@ -72,6 +72,9 @@ hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint3
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
+hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                            uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
+                            hipStream_t stream);
 
 // Slot i of the batch: frame = slot[offset : min(len, cap)].
 __global__ void __launch_bounds__(256)
@@ -284,15 +287,24 @@ int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t c
       (e = hipMemcpyAsync(s.d_start, s.h_off, (size_t)nb * 8, hipMemcpyHostToDevice, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(s.d_len, s.h_len, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
     return hip_error(e, "tx ring H2D");
-  if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess || (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring status reset");
-  if ((flags & LNX_TX_CHECKSUM) &&
-      (e = launch_tx_checksum(bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
-    return hip_error(e, "tx ring checksum launch");
-  if ((flags & LNX_TX_FCS) &&
-      (e = launch_fcs_append(bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
-          hipSuccess)
-    return hip_error(e, "tx ring FCS append launch");
+  if (direct) {
+    // frames in the pinned slots: one kernel reads each frame once over PCIe and
+    // stores only the fields, the padding and the FCS (rx_verify_kernel.hip tx_finish)
+    if ((e = launch_tx_finish(bytes, s.d_start, s.d_len, nb, capacity, flags, s.d_verdict, s.d_ok,
+                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "tx ring tx_finish launch");
+  } else {
+    if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess ||
+        (e = hipMemsetAsync(s.d_ok, 0, nb, s.s)) != hipSuccess)
+      return hip_error(e, "tx ring status reset");
+    if ((flags & LNX_TX_CHECKSUM) &&
+        (e = launch_tx_checksum(bytes, s.d_start, s.d_len, nb, s.d_verdict, r->num_cus, s.s)) != hipSuccess)
+      return hip_error(e, "tx ring checksum launch");
+    if ((flags & LNX_TX_FCS) &&
+        (e = launch_fcs_append(bytes, s.d_start, s.d_len, nb, capacity, s.d_ok, r->image, r->num_cus, s.s)) !=
+            hipSuccess)
+      return hip_error(e, "tx ring FCS append launch");
+  }
   if ((total && (e = hipMemcpyAsync(s.h_pack, s.d_bytes, total, hipMemcpyDeviceToHost, s.s)) != hipSuccess) ||
       (e = hipMemcpyAsync(s.h_len, s.d_len, (size_t)nb * 4, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
       (e = hipMemcpyAsync(s.h_ok, s.d_ok, nb, hipMemcpyDeviceToHost, s.s)) != hipSuccess ||
@@ -591,23 +603,18 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     if (rc != LNX_OK) break;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
     auto& s = r->st[sk];
-    // zero copy when the buffers are the ring's slots, in order and within one
-    // 2 GiB window (the transmit kernels' segment mode: non-decreasing starts,
-    // 31-bit offsets from the batch's first byte): the kernels patch them in place
+    // zero copy when the buffers are the ring's slots (any order): tx_finish
+    // reads each frame in place and patches it there
     bool direct = r->zero_copy;
-    uint64_t base = 0, prev = 0;
     for (uint32_t j = 0; j < nb && direct; ++j) {
       uint64_t pos = 0;
-      direct = in_ring(r, bufs[i0 + j], offset, capacity, &pos) && (j == 0 || pos >= prev + capacity) &&
-               pos + capacity - (j ? base : pos) < (1ull << 31) - 64;
-      if (j == 0) base = pos;
-      prev = pos;
-      s.h_off[j] = pos - base;
+      direct = in_ring(r, bufs[i0 + j], offset, capacity, &pos);
+      s.h_off[j] = pos;
       s.h_len[j] = lens[i0 + j];
     }
     if (direct) {
       in_place[sk] = true;
-      rc = enqueue_tx(r, s, nb, 0, capacity, flags, true, base);
+      rc = enqueue_tx(r, s, nb, 0, capacity, flags, true, 0);
       if (rc == LNX_OK) pending[sk] = {i0, nb}, r->stats.zero_copy_frames += nb;
       continue;
     }

@@ -162,50 +162,20 @@ constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 7
 constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead
 __device__ uint2 g_rv_zero[2];
 
-template <bool CRC, bool FILT>
-__global__ void __launch_bounds__(kRvBlock)
-rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
-                 uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
-                 const uint32_t* __restrict__ image, RxFilter filt) {
-  constexpr uint32_t kTabBytes = CRC ? kRvBytes : 0u;
-  constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
-  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
-  if constexpr (CRC) {
-    const uint32_t t = threadIdx.x;
-    for (uint32_t vi = t; vi < 2048u; vi += kRvBlock) {
-      const uint32_t v = image[vi];
-      uint4* row = reinterpret_cast<uint4*>(lds + kRvT + ((vi & 255u) << 8) + ((vi >> 8) << 5));
-      const uint4 v4 = {v, v, v, v};
-      row[0] = v4;
-      row[1] = v4;
-    }
-    // F_q (q < 32): entry e of table q at dword 32 e + q, so the 16 lanes of a
-    // row (16 different tables) read 16 different banks; B_b as in the image
-    for (uint32_t i = t; i < 32u * 128u; i += kRvBlock)
-      reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
-    for (uint32_t i = t; i < 8u * 128u; i += kRvBlock)
-      reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
-    __syncthreads();
-  }
-  const uint32_t trim = CRC ? 4u : 0u;
-  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4, wv = threadIdx.x >> 6;
-  const RvLane z(lane);
-  uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (FCS ok, S) per frame
-  uint2* head = res + kRvGroup;                                                // kRvHead qwords per frame
+// Phase A of a group (see above): kRvGroup / 4 passes of four 16-lane rows.
+// Lane k < kRvGroup holds its frame's start sk and length Ltk.  Per frame the
+// rows load the bytes [0, Ld), fold the CRC over them followed by zeros up to
+// Lc >= Ld, and sum the LE 16-bit words of [14, Ls):
+//   receive (TX = false): Ld = Lc = Ltk, Ls = Ltk - trim; res = (FCS ok, S);
+//   transmit (TX = true): Ld = Ls = Ltk, Lc = the length padded to 60 when the
+//     FCS is appended (Ltk otherwise); res = (the finished CRC register R of
+//     the frame as it is, S).
+// The frame's first kRvHead qwords go to head.
+template <bool CRC, bool TX>
+__device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head, const RvLane& z, const uint8_t* bytes,
+                                        uint64_t sk, uint32_t Ltk, uint32_t nrow, uint32_t trim, uint32_t capacity) {
+  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
   const uint2* zero = g_rv_zero;
-  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
-  for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
-    // the group's frames: lane k < kRvGroup holds frame g * kRvGroup + k's start and length (FCS included)
-    const uint64_t fk = g * kRvGroup + lane;
-    const bool live = lane < kRvGroup && fk < n;
-    const uint64_t fi = live ? fk : n - 1u;
-    const uint64_t sk = off[fi];
-    const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
-    const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
-    const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
-    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
-
-    // ---------------------------------------------------------------- A: data
     // the row's frame of pass j: its start (from the lane that holds it) and length
     auto row_frame = [&](uint32_t j, const uint8_t*& fr, uint32_t& Lt) {
       const uint32_t k = 4u * j + row;
@@ -234,12 +204,14 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     for (uint32_t j = 0; 4u * j < nrow; ++j) {
       const uint32_t k = 4u * j + row;  // the row's frame in the group
       const uint8_t* fr = frn;
+      // Lt: the bytes loaded and folded; Lc: the CRC's length (zeros past Lt); L: the sum's end
       const uint32_t Lt = Ltn;
-      const uint32_t L = Lt > trim ? Lt - trim : 0u;
+      const uint32_t Lc = TX && CRC && (Lt < 60u ? 60u : Lt) + 4u <= capacity ? (Lt < 60u ? 60u : Lt) : Lt;
+      const uint32_t L = TX ? Lt : (Lt > trim ? Lt - trim : 0u);
       const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
       const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
       const int32_t QE = (int32_t)((Lt + mis + 7u) >> 3);  // qwords holding frame bytes
-      const int32_t NL = (QE + 15) >> 4;                   // lines of the window
+      const int32_t NL = (int32_t)(((Lc + mis + 7u) >> 3) + 15u) >> 4;  // lines of the CRC window
       int32_t nit = (QE + 16 * kRvUnroll - 1) / (16 * kRvUnroll), qmin = QE;
       nit = max(nit, __shfl_xor(nit, 16));
       nit = max(nit, __shfl_xor(nit, 32));
@@ -256,7 +228,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
           const int32_t o0 = 8 * (int32_t)p - (int32_t)mis;
           S = rv_dot2(c0 & rv_keep_from(14 - o0), rv_dot2(c1 & rv_keep_from(10 - o0), S));
           if constexpr (CRC) {
-            const int32_t ie = (int32_t)(Lt < 4 ? Lt : 4u);
+            const int32_t ie = (int32_t)(Lc < 4 ? Lc : 4u);
             c0 = (c0 & rv_range(o0, 0, (int32_t)Lt)) ^ rv_range(o0, 0, ie);
             c1 = (c1 & rv_range(o0 + 4, 0, (int32_t)Lt)) ^ rv_range(o0 + 4, 0, ie);
           }
@@ -283,7 +255,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
           prefetch(frn, Ltn);
         }
         if (p < kRvHead) head[kRvHead * k + p] = y[0];  // the frame's first qwords for phase B
-        if (qmin >= 16 * (kRvUnroll - 1) + 1) {
+        if (qmin >= 16 * (kRvUnroll - 1) + 1) {  // (then NL >= 12: Lc >= Lt)
           // every row's window covers all twelve lines (MTU frames): no window test
 #pragma unroll
           for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, 0, true);
@@ -316,16 +288,63 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
         const bool junk = qme == lastq && lastq >= 16;
         r ^= rv_unit(lds, junk ? ye.x & rv_keep_from((int32_t)Lt - oe) : 0u,
                      junk ? ye.y & rv_keep_from((int32_t)Lt - oe - 4) : 0u, z);
-        // the window ends W = 128 NL - mis (frame offsets) past the frame start; W - Lt = 8a + b
-        const uint32_t pad = (uint32_t)(128 * NL - (int32_t)mis - (int32_t)Lt);
+        // the window ends W = 128 NL - mis (frame offsets) past the frame start; W - Lc = 8a + b
+        const uint32_t pad = (uint32_t)(128 * NL - (int32_t)mis - (int32_t)Lc);
         const uint32_t a = pad >> 3, b = pad & 7u;
         const uint32_t x = rv_row_xor(rv_nib_f(lds, p + a, r));
         const uint32_t R = rv_nib(lds, kRvB + 512u * b, x);
-        okf = Lt >= 4 && ~R == 0x2144DF1Cu;
+        okf = TX ? R : (uint32_t)(Lt >= 4 && ~R == 0x2144DF1Cu);
       }
       S = rv_row_add(S);
       if (p == 0) res[k] = make_uint2(okf, S);
     }
+}
+
+template <bool CRC, bool FILT>
+__global__ void __launch_bounds__(kRvBlock)
+rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
+                 uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
+                 const uint32_t* __restrict__ image, RxFilter filt) {
+  constexpr uint32_t kTabBytes = CRC ? kRvBytes : 0u;
+  constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
+  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
+  if constexpr (CRC) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t vi = t; vi < 2048u; vi += kRvBlock) {
+      const uint32_t v = image[vi];
+      uint4* row = reinterpret_cast<uint4*>(lds + kRvT + ((vi & 255u) << 8) + ((vi >> 8) << 5));
+      const uint4 v4 = {v, v, v, v};
+      row[0] = v4;
+      row[1] = v4;
+    }
+    // F_q (q < 32): entry e of table q at dword 32 e + q, so the 16 lanes of a
+    // row (16 different tables) read 16 different banks; B_b as in the image
+    for (uint32_t i = t; i < 32u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
+    for (uint32_t i = t; i < 8u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
+    __syncthreads();
+  }
+  const uint32_t trim = CRC ? 4u : 0u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const RvLane z(lane);
+  uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (FCS ok, S) per frame
+  uint2* head = res + kRvGroup;                                                // kRvHead qwords per frame
+  const uint2* zero = g_rv_zero;
+  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
+    // the group's frames: lane k < kRvGroup holds frame g * kRvGroup + k's start and length (FCS included)
+    const uint64_t fk = g * kRvGroup + lane;
+    const bool live = lane < kRvGroup && fk < n;
+    const uint64_t fi = live ? fk : n - 1u;
+    const uint64_t sk = off[fi];
+    const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
+    const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
+    const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
+    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+
+    // ---------------------------------------------------------------- A: data
+    rv_rows<CRC, false>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
     __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, read back in order below)
 
     // ---------------------------------------------------------------- B: verdicts
@@ -570,6 +589,313 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     }
     __builtin_amdgcn_wave_barrier();  // the next group rewrites res and head
   }
+}
+
+// ------------------------------------------------------------------ transmit
+// tx_finish_kernel: lneto's transmit tail for frames in place, ONE read of each
+// frame -- the checksum-generate step (lnx_tx_checksum_batch: encapsulate4 /
+// encapsulate6 and the ICMP clients, internet/stack-ip4.go:202-228,
+// internet/stack-ip6.go:167-181, ipv4/icmpv4/client.go:210-214,
+// ipv6/icmpv6/client.go:135-148; ingress_kernel.hip GEN) and then the padding
+// to 60 bytes and the LE FCS (lnx_fcs_append_batch, internet/stack-ethernet.go:
+// 200-214).  Phase A is the receive kernel's (rv_rows<CRC, true>): the raw sum
+// S of [14, L) and the CRC register R0 of the frame AS IT IS, padded with
+// zeros.  Phase B, one lane per frame, parses the headers, sets the length
+// fields and checksums exactly as the GEN rows do (sums over the bytes as
+// loaded, the old field values taken out), and corrects the CRC for the fields
+// it changed by linearity: a 16-bit change d at frame offset o changes the
+// register after Lp bytes by Z_{Lp - o}(d) (d's first byte in the register's
+// low byte); all such fields lie in the first 128 bytes, so
+//   R = R0 ^ Z_{Lp - c}( XOR_f Z_{c - o_f}(d_f) ),  c = min(Lp, 128),
+// the shifts by binary powers (nibble tables of Z_{2^m}, m < 16: every frame
+// the step changes is shorter than 64 KiB).  Then the fields, the padding and
+// the FCS are stored in place: a few 2- and 4-byte stores per frame, which is
+// what the zero-copy egress of the ring wants (each store to host memory costs
+// about a nanosecond, tools/ubench/host_write.hip).
+// Segment form: frame f = bytes[start[f] : start[f] + len[f]], with room for
+// the padding and FCS within `capacity` bytes of start[f]; len[f] is updated;
+// st_ck[f] = the checksum step's status (0, 18, 15), st_ap[f] = the append's
+// (0, or 6 ErrShortBuffer with the frame left unpadded).
+constexpr uint32_t kTxP = kRvBytes;                    // Z_{2^m} nibble tables in LDS (after F, B)
+constexpr uint32_t kTxTabBytes = kRvBytes + 16u * 512u;
+constexpr uint32_t kTxImgP = kRvImgF + 40u * 128u;     // ... and in the image
+
+// Z_k(x), k < 2^16, by binary powers (the steps some lane of the wave needs)
+__device__ __forceinline__ uint32_t tx_zk(const char* lds, uint32_t k, uint32_t x) {
+#pragma unroll 1
+  for (uint32_t m = 0; m < 16u; ++m) {
+    if (__builtin_amdgcn_ballot_w64((k >> m) & 1u) == 0) continue;
+    const uint32_t y = rv_nib(lds, kTxP + 512u * m, x);
+    x = (k >> m) & 1u ? y : x;
+  }
+  return x;
+}
+
+// store the big-endian 16-bit value v at frame address q (2 bytes)
+__device__ __forceinline__ void tx_put16(uint8_t* q, uint32_t v) {
+  if ((reinterpret_cast<uintptr_t>(q) & 1u) == 0) {
+    *reinterpret_cast<uint16_t*>(q) = (uint16_t)(((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu));
+  } else {
+    q[0] = (uint8_t)(v >> 8);
+    q[1] = (uint8_t)v;
+  }
+}
+// store the 4 bytes of w (little-endian) at q, by naturally aligned pieces
+__device__ __forceinline__ void tx_put32(uint8_t* q, uint32_t w) {
+  const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 3u);
+  if (a == 0) {
+    *reinterpret_cast<uint32_t*>(q) = w;
+  } else if (a == 2) {
+    reinterpret_cast<uint16_t*>(q)[0] = (uint16_t)w;
+    reinterpret_cast<uint16_t*>(q)[1] = (uint16_t)(w >> 16);
+  } else {
+    q[0] = (uint8_t)w;
+    *reinterpret_cast<uint16_t*>(q + 1) = (uint16_t)(w >> 8);
+    q[3] = (uint8_t)(w >> 24);
+  }
+}
+
+template <bool FCS, bool CK>
+__global__ void __launch_bounds__(kRvBlock)
+tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
+                 uint64_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
+                 const uint32_t* __restrict__ image) {
+  constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
+  constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
+  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
+  if constexpr (FCS) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t vi = t; vi < 2048u; vi += kRvBlock) {
+      const uint32_t v = image[vi];
+      uint4* row = reinterpret_cast<uint4*>(lds + kRvT + ((vi & 255u) << 8) + ((vi >> 8) << 5));
+      const uint4 v4 = {v, v, v, v};
+      row[0] = v4;
+      row[1] = v4;
+    }
+    for (uint32_t i = t; i < 32u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
+    for (uint32_t i = t; i < 8u * 128u; i += kRvBlock)
+      reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
+    for (uint32_t i = t; i < 16u * 128u; i += kRvBlock) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const RvLane z(lane);
+  uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (R0, S) per frame
+  uint2* head = res + kRvGroup;
+  const uint2* zero = g_rv_zero;
+  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
+    const uint64_t fk = g * kRvGroup + lane;
+    const bool live = lane < kRvGroup && fk < n;
+    const uint64_t fi = live ? fk : n - 1u;
+    const uint64_t sk = start[fi];
+    const uint32_t Ltk = live ? len[fi] : 0u;
+    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+    rv_rows<FCS, true>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---------------------------------------------------------------- B: one lane per frame
+    const uint32_t L = Ltk;
+    uint8_t* fr = bytes + sk;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
+    const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
+    const int32_t QE = (int32_t)((L + mis + 7u) >> 3);
+    const uint32_t kk = lane < kRvGroup ? lane : 0u;
+    uint32_t dw[22];
+#pragma unroll
+    for (uint32_t i = 0; i < kRvHead; ++i) {
+      const uint2 v = head[kRvHead * kk + i];
+      dw[2 * i] = v.x;
+      dw[2 * i + 1] = v.y;
+    }
+    const uint32_t sh = mis & 3u;
+    uint32_t F[15];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const uint32_t lo = mis >= 4 ? dw[k + 1] : dw[k], hi = mis >= 4 ? dw[k + 2] : dw[k + 1];
+      F[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+    auto byt = [](uint32_t w, int i) -> uint32_t { return (w >> (8 * i)) & 0xFFu; };
+    auto be16 = [&](int o) -> uint32_t {
+      const uint32_t w = (o & 3) == 3 ? __builtin_amdgcn_alignbyte(F[(o >> 2) + 1], F[o >> 2], 3) : F[o >> 2];
+      const int i = (o & 3) == 3 ? 0 : (o & 3);
+      return (byt(w, i) << 8) | byt(w, i + 1);
+    };
+    auto dyn16 = [&](uint32_t o) -> uint32_t {  // (o + 2 <= L checked by the caller)
+      const uint32_t a = o + mis;
+      uint32_t b0, b1;
+      if (a + 2u <= 8u * kRvHead) {
+        const uint8_t* hb = reinterpret_cast<const uint8_t*>(head + kRvHead * kk);
+        b0 = hb[a];
+        b1 = hb[a + 1u];
+      } else {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(base2) + (a >> 2);
+        const uint32_t lo = rv_ld32(w), hi = (a & 3u) == 3u ? rv_ld32(w + 1) : 0u;
+        const uint32_t v2 = __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
+        b0 = v2 & 0xFFu;
+        b1 = (v2 >> 8) & 0xFFu;
+      }
+      return (b0 << 8) | b1;
+    };
+    auto hsum = [&](auto D0, auto D1, int32_t a, int32_t b) -> uint32_t {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int d = decltype(D0)::value; d < decltype(D1)::value; ++d)
+        acc = rv_dot2(dw[d] & rv_range(4 * d - (int32_t)mis, a, b), acc);
+      return acc;
+    };
+    using I3 = std::integral_constant<int, 3>;
+    using I5 = std::integral_constant<int, 5>;
+    using I11 = std::integral_constant<int, 11>;
+    using I16 = std::integral_constant<int, 16>;
+    using I22 = std::integral_constant<int, 22>;
+    // a 16-bit big-endian value at an even frame offset, as it adds to the LE half-word sums
+    auto cv = [&](uint32_t v) -> uint32_t { return (mis & 1u) ? v : (((v & 0xFFu) << 8) | (v >> 8)); };
+
+    // ---- the checksum step (ingress_kernel.hip GEN, oracle.tx_checksum)
+    uint32_t v = 0;
+    uint32_t g_off[4] = {0, 0, 0, 0}, g_new[4] = {0, 0, 0, 0}, g_old[4] = {0, 0, 0, 0};
+    bool hdr_sum = false, l4_sum = false, g_nz = false;
+    int32_t pa = 0, pb = 0, la = 0;
+    uint32_t lseed = 0, g_fix_h = 0, g_fix_t = 0;
+    if constexpr (CK) {
+      if (L < 14) {
+        v = kErrTruncatedFrame;
+      } else {
+        const uint32_t et = be16(12);
+        if (et == 0x0800) {
+          const uint32_t ihl = byt(F[3], 2) & 15u, hl = 4 * ihl;
+          if (L < 34) v = kErrTruncatedFrame;
+          else if (ihl < 5) v = kErrInvalidLengthField;
+          else if (14 + hl > L) v = kErrTruncatedFrame;
+          else if (L - 14 > 0xFFFFu) v = kErrInvalidLengthField;
+          if (v == 0) {
+            const uint32_t tl = L - 14, nn = tl - hl, proto = byt(F[5], 3);
+            const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 1) ? 8u : 0u;
+            if (nn < need) v = kErrTruncatedFrame;
+            if (v == 0) {
+              hdr_sum = true;
+              g_off[0] = 16, g_new[0] = tl, g_old[0] = be16(16);  // SetTotalLength(n + hl)
+              g_off[1] = 24, g_old[1] = be16(24);                 // SetCRC(CalculateHeaderCRC())
+              g_fix_h = cv(tl) - cv(g_old[0]) - cv(g_old[1]);
+              if (need) {
+                l4_sum = true;
+                la = 14 + hl;
+                const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
+                g_off[2] = la + at, g_old[2] = dyn16(la + at);
+                g_fix_t = 0u - cv(g_old[2]);
+                if (proto != 1) pa = 26, pb = 34, lseed = nn + proto;  // CRCWriteTCPPseudo / CRCWriteUDPPseudo(n)
+                if (proto == 17) {
+                  g_off[3] = la + 4, g_new[3] = nn, g_old[3] = dyn16(la + 4);  // SetLength(n)
+                  g_fix_t += cv(nn) - cv(g_old[3]);
+                  g_nz = true;
+                }
+              }
+            }
+          }
+        } else if (et == 0x86DD) {
+          const uint32_t nn = L - 54, proto = byt(F[5], 0);
+          if (L < 54) v = kErrTruncatedFrame;
+          else if (nn > 0xFFFFu) v = kErrInvalidLengthField;
+          const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 58) ? 8u : 0u;
+          if (v == 0 && nn < need) v = kErrTruncatedFrame;
+          if (v == 0) {
+            g_off[0] = 18, g_new[0] = nn, g_old[0] = be16(18);  // SetPayloadLength(n)
+            if (need) {
+              l4_sum = true;
+              pa = 22, pb = 54, la = 54;  // CRCWritePseudo: AddUint32(n), AddUint32(proto)
+              lseed = nn + proto;
+              const uint32_t at = proto == 6 ? 16u : proto == 17 ? 6u : 2u;
+              g_off[2] = 54 + at, g_old[2] = dyn16(54 + at);
+              g_fix_t = 0u - cv(g_old[2]);
+              if (proto == 17) {
+                g_off[3] = 58, g_new[3] = nn, g_old[3] = be16(58);
+                g_fix_t += cv(nn) - cv(g_old[3]);
+                g_nz = true;
+              }
+            }
+          }
+        }
+      }
+      // IPv4 options past the staged bytes: qwords 9 and 10 from memory
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int32_t q = (int32_t)kRvHead + i;
+        const bool need = l4_sum && la + (int32_t)mis > 8 * (int32_t)kRvHead && q < QE;
+        const uint2 v2 = rv_ld(need ? base2 + q : zero);
+        dw[2 * q] = v2.x;
+        dw[2 * q + 1] = v2.y;
+      }
+      const uint2 rk = res[kk];
+      auto conv = [&](uint32_t S) -> uint32_t {
+        if (mis & 1u) return S;
+        uint32_t fo = (S & 0xFFFFu) + (S >> 16);
+        fo = (fo & 0xFFFFu) + (fo >> 16);
+        return ((fo << 8) | (fo >> 8)) & 0xFFFFu;
+      };
+      if (hdr_sum) g_new[1] = rv_sum16(conv(hsum(I3{}, I11{}, 14, 34) + g_fix_h)) & 0xFFFFu;
+      if (l4_sum) {
+        const uint32_t tS = rk.y - hsum(I3{}, I22{}, 14, la) + hsum(I5{}, I16{}, pa, pb) + g_fix_t;
+        const uint32_t tc = rv_sum16(conv(tS) + lseed) & 0xFFFFu;
+        g_new[2] = g_nz && tc == 0 ? 0xFFFFu : tc;
+      }
+    }
+    const bool written = CK && v == 0;
+
+    // ---- the FCS over the frame with its new fields, padded to 60 bytes
+    const uint32_t Lp = L < 60u ? 60u : L;
+    const bool app = FCS && Lp + 4u <= capacity;
+    uint32_t fcs = 0;
+    if constexpr (FCS) {
+      const uint32_t c = Lp < 128u ? Lp : 128u;
+      uint32_t D = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t d = written && g_off[i] != 0 ? (g_old[i] ^ g_new[i]) : 0u;
+        const uint32_t dl = ((d >> 8) & 0xFFu) | ((d & 0xFFu) << 8);  // the field's first byte low
+        D ^= tx_zk(lds, app && dl ? c - g_off[i] : 0u, dl);
+      }
+      const uint32_t dR = tx_zk(lds, app ? Lp - c : 0u, D);
+      fcs = ~(res[kk].x ^ dR);
+    }
+
+    // ---- stores: the fields, the padding, the FCS; the length and statuses
+    if (live) {
+      if (written) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (g_off[i] != 0) tx_put16(fr + g_off[i], g_new[i]);
+      }
+      if (app) {
+        for (uint32_t o = L; o < Lp; ++o) fr[o] = 0;  // runts: zero padding to 60 bytes
+        tx_put32(fr + Lp, fcs);
+      }
+      len[fk] = app ? Lp + 4u : L;
+      st_ck[fk] = (uint8_t)v;
+      st_ap[fk] = (uint8_t)(FCS && !app ? 6u : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                            uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
+                            hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
+  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+  const bool ck = flags & 1u, fcs = flags & 2u;
+#define LNX_TX(A, C)                                                                                               \
+  hipLaunchKernelGGL((tx_finish_kernel<A, C>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, start, len, n, \
+                     capacity, st_ck, st_ap, image)
+  if (fcs) {
+    if (ck) LNX_TX(true, true); else LNX_TX(true, false);
+  } else {
+    if (ck) LNX_TX(false, true); else LNX_TX(false, false);
+  }
+#undef LNX_TX
+  return hipGetLastError();
 }
 
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,

@@ -388,8 +388,8 @@ def test_packets_on_ring_slots(cuda, offset):
     ring's slots (x/netdev/runner.go:92-94), so IngressPackets / EgressPackets
     get views of the ring's pinned memory and the kernels read (egress: patch)
     the frames in place.  Against the oracle, with the copying path on the same
-    frames, and with the cases that must fall back to staging: a buffer outside
-    the ring, egress buffers out of slot order."""
+    frames, with a buffer outside the ring (that batch is staged) and egress
+    buffers out of slot order."""
     from tests.test_tx_checksum import tx_frames
     rx = _case_frames(seed=70 + offset, count=700)
     cap = max(1536, _cap_for(rx, offset))
@@ -425,7 +425,7 @@ def test_packets_on_ring_slots(cuda, offset):
             s0 = ring.stats()["zero_copy_frames"]
             sizes, status = ring.egress_packets(bufs, [len(tx[i]) for i in idx], offset=offset, capacity=capacity)
             zc = ring.stats()["zero_copy_frames"] - s0
-            assert zc == (len(tx) if order == "slots" else 0), (order, zc)
+            assert zc == len(tx), (order, zc)  # slot buffers in any order are patched in place
             bad = []
             for k, i in enumerate(idx):
                 want, st = O.tx_checksum(tx[i])
@@ -436,5 +436,51 @@ def test_packets_on_ring_slots(cuda, offset):
                 assert np.array_equal(ring.slots[i, :offset], junk[i, :offset])
                 assert np.array_equal(ring.slots[i, offset + len(want):], junk[i, offset + len(want):]), (order, i)
             assert not bad, bad[:10]
+    finally:
+        ring.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [L.TX_CHECKSUM | L.TX_FCS, L.TX_FCS, L.TX_CHECKSUM])
+@pytest.mark.parametrize("offset", [0, 3])
+def test_egress_in_place_matches_oracle(cuda, flags, offset):
+    """Zero-copy egress (tx_finish_kernel, rx_verify_kernel.hip): frames written
+    into the ring's slots, finished in place by one kernel that reads each frame
+    once -- checksum generate (oracle.tx_checksum) with the CRC corrected for
+    the fields it writes, then the padding and FCS (oracle.fcs_append) -- for
+    every protocol the step knows, runts, frames too short, and frames whose
+    padded length does not fit `capacity` (ErrShortBuffer)."""
+    from tests.test_tx_checksum import tx_frames
+    cap = 2048
+    frames = [f for f in tx_frames(seed=70 + offset, count=1400) if len(f) <= 1900]
+    rng = np.random.default_rng(71)
+    ring = _ring(len(frames), slot_cap=cap, batch_slots=256, depth=3)
+    try:
+        junk = rng.integers(0, 256, (len(frames), cap), dtype=np.uint8)
+        ring.slots[:] = junk
+        caps = []
+        for i, f in enumerate(frames):
+            ring.slots[i, offset:offset + len(f)] = np.frombuffer(f, np.uint8)
+            caps.append(cap - offset)
+        # FCS only: a capacity 2 bytes over the longest frame, which then does not fit
+        capacity = cap - offset if flags != L.TX_FCS else max(len(f) for f in frames) + 2
+        s0 = ring.stats()["zero_copy_frames"]
+        sizes, status = ring.egress_packets([ring.slots[i] for i in range(len(frames))], [len(f) for f in frames],
+                                            offset=offset, capacity=capacity, flags=flags)
+        assert ring.stats()["zero_copy_frames"] - s0 == len(frames)
+        bad = []
+        for i, f in enumerate(frames):
+            want, st = O.tx_checksum(f) if flags & L.TX_CHECKSUM else (f, 0)
+            st2 = 0
+            if flags & L.TX_FCS:
+                want, st2 = O.fcs_append(want, capacity)
+            got = ring.slots[i, offset:offset + int(sizes[i])].tobytes()
+            if got != want or int(status[i]) != (st or st2):
+                bad.append((i, len(f), int(sizes[i]), len(want), int(status[i]), st or st2))
+            assert np.array_equal(ring.slots[i, :offset], junk[i, :offset])
+            assert np.array_equal(ring.slots[i, offset + len(want):], junk[i, offset + len(want):]), i
+        assert not bad, bad[:10]
+        if flags == L.TX_FCS:
+            assert (status == 6).sum() >= 1  # frames past the capacity stay unpadded
     finally:
         ring.close()
