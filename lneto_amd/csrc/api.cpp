@@ -34,7 +34,7 @@ hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* l
 #endif
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream);
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
                                  uint32_t trim, const RxFilter* filter);

@@ -56,7 +56,7 @@ namespace lnx {
 int device_resources(const void** image, int* num_cus, const void** stage_image, const void** rx_image);
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream);
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false);
 int hip_error(hipError_t e, const char* what);
 // host_path.cpp: the per-frame host forms (batches below the ring's host threshold)
 uint8_t host_verdict(const uint8_t* fr, size_t L, uint32_t flags, const RxFilter& f);
@@ -230,7 +230,7 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, RxSrc src, uint32_t b0, ui
         (e = hipMemcpyAsync(s.d_len, s.h_len, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
       return hip_error(e, "rx ring H2D (frame table)");
     if ((e = launch_rx_verify(r->d_slots, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict, s.d_len, &r->filt,
-                              rx_image, r->num_cus, s.s)) != hipSuccess)
+                              rx_image, r->num_cus, s.s, true)) != hipSuccess)
       return hip_error(e, "rx ring rx_verify launch");
   } else if (src == RxSrc::kSlotsDirect) {
     if ((e = hipMemcpyAsync(s.d_len, r->h_len + b0, (size_t)nb * 4, hipMemcpyHostToDevice, s.s)) != hipSuccess)
@@ -239,7 +239,7 @@ int enqueue_rx(lnx_rx_ring* r, Stage& s, uint32_t nb, RxSrc src, uint32_t b0, ui
     hipLaunchKernelGGL(ring_segments_kernel, dim3(grid), dim3(256), 0, s.s, s.d_start, s.d_len, nb, r->cap, offset);
     if ((e = hipGetLastError()) != hipSuccess) return hip_error(e, "ring_segments_kernel launch");
     if ((e = launch_rx_verify(r->d_slots + (size_t)b0 * r->cap, s.d_start, nb, vflags, fcs, s.d_ok, s.d_verdict,
-                              s.d_len, &r->filt, rx_image, r->num_cus, s.s)) != hipSuccess)
+                              s.d_len, &r->filt, rx_image, r->num_cus, s.s, true)) != hipSuccess)
       return hip_error(e, "rx ring rx_verify launch");
   } else if (src == RxSrc::kPacked) {
     const uint64_t total = s.h_off[nb];

@@ -170,8 +170,10 @@ __device__ uint2 g_rv_zero[2];
 //   transmit (TX = true): Ld = Ls = Ltk, Lc = the length padded to 60 when the
 //     FCS is appended (Ltk otherwise); res = (the finished CRC register R of
 //     the frame as it is, S).
-// The frame's first kRvHead qwords go to head.
-template <bool CRC, bool TX>
+// The frame's first kRvHead qwords go to head.  HOST (frames in pinned host
+// memory, read over PCIe): the qwords past the frame's end are captured as the
+// fold passes them instead of loaded again (a second PCIe round trip).
+template <bool CRC, bool TX, bool HOST>
 __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head, const RvLane& z, const uint8_t* bytes,
                                         uint64_t sk, uint32_t Ltk, uint32_t nrow, uint32_t trim, uint32_t capacity) {
   const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
@@ -184,28 +186,31 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       Lt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ltk);
       fr = bytes + (((uint64_t)shi << 32) | slo);
     };
-    // the first kRvPf qwords of a pass's batch 0 are loaded during the pass before
-    // (software pipelining: their latency overlaps the previous frame's fold)
-    uint2 pf[kRvPf];
-    const uint8_t* frn;
-    uint32_t Ltn;
-    row_frame(0, frn, Ltn);
-    auto prefetch = [&](const uint8_t* f2, uint32_t L2) {
-      const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(f2) & 7u);
-      const uint2* b2 = reinterpret_cast<const uint2*>(f2 - m2);
-      const int32_t Q2 = (int32_t)((L2 + m2 + 7u) >> 3);
+    // the first PQ qwords of a pass's batch 0 are loaded PR passes before
+    // (software pipelining: their latency overlaps the previous frames' folds)
+    constexpr int PR = 1, PQ = kRvPf;  // (two passes ahead for host memory measured no faster: 33.8 against 35-37 GiB/s)
+    uint2 pf[PR][PQ];
+    const uint8_t* frn[PR];
+    uint32_t Ltn[PR];
+    auto prefetch = [&](int slot, uint32_t jn) {
+      if (4u * jn >= nrow) return;  // (wave-uniform)
+      row_frame(jn, frn[slot], Ltn[slot]);
+      const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(frn[slot]) & 7u);
+      const uint2* b2 = reinterpret_cast<const uint2*>(frn[slot] - m2);
+      const int32_t Q2 = (int32_t)((Ltn[slot] + m2 + 7u) >> 3);
 #pragma unroll
-      for (int u = 0; u < kRvPf; ++u) {
+      for (int u = 0; u < PQ; ++u) {
         const int32_t q = (int32_t)p + 16 * u;
-        pf[u] = rv_ld(q < Q2 ? b2 + q : zero);
+        pf[slot][u] = rv_ld(q < Q2 ? b2 + q : zero);
       }
     };
-    prefetch(frn, Ltn);
+#pragma unroll
+    for (int a = 0; a < PR; ++a) prefetch(a, (uint32_t)a);
     for (uint32_t j = 0; 4u * j < nrow; ++j) {
       const uint32_t k = 4u * j + row;  // the row's frame in the group
-      const uint8_t* fr = frn;
+      const uint8_t* fr = frn[0];
       // Lt: the bytes loaded and folded; Lc: the CRC's length (zeros past Lt); L: the sum's end
-      const uint32_t Lt = Ltn;
+      const uint32_t Lt = Ltn[0];
       const uint32_t Lc = TX && CRC && (Lt < 60u ? 60u : Lt) + 4u <= capacity ? (Lt < 60u ? 60u : Lt) : Lt;
       const uint32_t L = TX ? Lt : (Lt > trim ? Lt - trim : 0u);
       const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
@@ -220,6 +225,23 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       qmin = min(qmin, __shfl_xor(qmin, 32));
       qmin = __builtin_amdgcn_readfirstlane(qmin);
       uint32_t r = 0, S = 0;
+      // the qwords holding the bytes at or past L (the FCS, the last qword's
+      // bytes past the frame) went into S, those past Lt into the CRC of lines
+      // >= 1: the lanes that hold them (qwords qL .. QE - 1, at most two) take
+      // them out again after the fold
+      const int32_t lastq = QE - 1, qL = (int32_t)((L + mis) >> 3);
+      const int32_t qme = (lastq & 15) == (int32_t)p ? lastq : (qL & 15) == (int32_t)p && qL < lastq ? qL : -1;
+      uint2 ye = make_uint2(0u, 0u);
+      auto capture = [&](const uint2 (&y)[kRvUnroll], int it) {
+        if constexpr (HOST) {
+#pragma unroll
+          for (int u = 0; u < kRvUnroll; ++u) {
+            const bool at = (int32_t)p + 16 * (u + kRvUnroll * it) == qme;
+            ye.x = at ? y[u].x : ye.x;
+            ye.y = at ? y[u].y : ye.y;
+          }
+        }
+      };
       // one qword: the sum, and the CRC unit (in the window iff `in`)
       auto fold = [&](uint2 y, int u, int it, bool in) {
         uint32_t c0 = y.x, c1 = y.y;
@@ -244,17 +266,23 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
         // batch 0: the prefetched qwords, the rest loaded now, then the next pass's prefetch
         uint2 y[kRvUnroll];
 #pragma unroll
-        for (int u = 0; u < kRvPf; ++u) y[u] = pf[u];
+        for (int u = 0; u < PQ; ++u) y[u] = pf[0][u];
 #pragma unroll
-        for (int u = kRvPf; u < kRvUnroll; ++u) {
+        for (int u = PQ; u < kRvUnroll; ++u) {
           const int32_t q = (int32_t)p + 16 * u;
           y[u] = rv_ld(q < QE ? base2 + q : zero);
         }
-        if (4u * (j + 1u) < nrow) {
-          row_frame(j + 1u, frn, Ltn);
-          prefetch(frn, Ltn);
+        // the prefetch slots move down one; the last takes pass j + PR
+#pragma unroll
+        for (int a = 0; a + 1 < PR; ++a) {
+          frn[a] = frn[a + 1];
+          Ltn[a] = Ltn[a + 1];
+#pragma unroll
+          for (int u = 0; u < PQ; ++u) pf[a][u] = pf[a + 1][u];
         }
+        prefetch(PR - 1, j + (uint32_t)PR);
         if (p < kRvHead) head[kRvHead * k + p] = y[0];  // the frame's first qwords for phase B
+        capture(y, 0);
         if (qmin >= 16 * (kRvUnroll - 1) + 1) {  // (then NL >= 12: Lc >= Lt)
           // every row's window covers all twelve lines (MTU frames): no window test
 #pragma unroll
@@ -271,15 +299,11 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
           const int32_t q = (int32_t)p + 16 * (u + kRvUnroll * it);
           y[u] = rv_ld(q < QE ? base2 + q : zero);
         }
+        capture(y, it);
 #pragma unroll
         for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, it, u + kRvUnroll * it < NL);
       }
-      // the bytes at or past L (the FCS, the last qword's bytes past the frame)
-      // went into S, those past Lt into the CRC of lines >= 1: the lanes that
-      // hold them (qwords qL .. QE - 1, at most two) take them out again
-      const int32_t lastq = QE - 1, qL = (int32_t)((L + mis) >> 3);
-      const int32_t qme = (lastq & 15) == (int32_t)p ? lastq : (qL & 15) == (int32_t)p && qL < lastq ? qL : -1;
-      const uint2 ye = rv_ld(qme >= 0 ? base2 + qme : zero);
+      if constexpr (!HOST) ye = rv_ld(qme >= 0 ? base2 + qme : zero);  // (an L2 hit: the fold just read it)
       const int32_t oe = 8 * qme - (int32_t)mis;
       S -= rv_dot2(ye.x & rv_keep_from((int32_t)L - oe), rv_dot2(ye.y & rv_keep_from((int32_t)L - oe - 4), 0u)) &
            (qme >= 0 && L >= 14 ? ~0u : 0u);
@@ -300,7 +324,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
     }
 }
 
-template <bool CRC, bool FILT>
+template <bool CRC, bool FILT, bool HOST>
 __global__ void __launch_bounds__(kRvBlock)
 rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
                  uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
@@ -344,7 +368,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
 
     // ---------------------------------------------------------------- A: data
-    rv_rows<CRC, false>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
+    rv_rows<CRC, false, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
     __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, read back in order below)
 
     // ---------------------------------------------------------------- B: verdicts
@@ -692,7 +716,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
     const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
-    rv_rows<FCS, true>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
+    rv_rows<FCS, true, true>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);  // (the ring's slots)
     __builtin_amdgcn_wave_barrier();
 
     // ---------------------------------------------------------------- B: one lane per frame
@@ -900,19 +924,27 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
 
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream) {
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host) {
   RxFilter filt{};
   if (filter) filt = *filter;
   if (n == 0) return hipSuccess;
   uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
-#define LNX_RV(C, F)                                                                                       \
-  hipLaunchKernelGGL((rx_verify_kernel<C, F>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, off, n, \
+#define LNX_RV(C, F, H)                                                                                       \
+  hipLaunchKernelGGL((rx_verify_kernel<C, F, H>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, off, n, \
                      flags, ok, verdict, seg_len, image, filt)
-  if (fcs) {
-    if (filt.on) LNX_RV(true, true); else LNX_RV(true, false);
+  if (host) {
+    if (fcs) {
+      if (filt.on) LNX_RV(true, true, true); else LNX_RV(true, false, true);
+    } else {
+      if (filt.on) LNX_RV(false, true, true); else LNX_RV(false, false, true);
+    }
   } else {
-    if (filt.on) LNX_RV(false, true); else LNX_RV(false, false);
+    if (fcs) {
+      if (filt.on) LNX_RV(true, true, false); else LNX_RV(true, false, false);
+    } else {
+      if (filt.on) LNX_RV(false, true, false); else LNX_RV(false, false, false);
+    }
   }
 #undef LNX_RV
   return hipGetLastError();

@@ -6,6 +6,8 @@
 //   mode 2: one 16-byte store
 //   mode 3: 64 contiguous bytes per slot by 4 adjacent lanes (16 B each)
 //   mode 4: read 256 B per slot (16 lanes x 16 B), no store (the read side)
+//   mode 5-7: the same 256 B as 32 lanes x 8 B, 16 lanes x 2 x 8 B (the receive
+//           rows' pattern), 8 lanes x 2 x 16 B
 // by one lane per slot (modes 0-2) or as stated, with hipEvent timing.
 //   hipcc --offload-arch=gfx950 -O3 tools/ubench/host_write.hip -o tools/ubench/host_write
 #include <hip/hip_runtime.h>
@@ -33,12 +35,60 @@ __global__ void patch(uint8_t* __restrict__ slots, uint32_t n, uint32_t cap, int
     const uint32_t f = t >> 2, q = t & 3u;
     if (f >= n) return;
     *reinterpret_cast<uint4*>(slots + (size_t)f * cap + 16u * q) = make_uint4(t, t + 1, t + 2, t + 3);
-  } else {
+  } else if (mode == 4) {
     const uint32_t f = t >> 4, q = t & 15u;
     if (f >= n) return;
     const uint4 v = *reinterpret_cast<const uint4*>(slots + (size_t)f * cap + 16u * q);
     if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) sink[0] = t;
+  } else if (mode == 5) {  // 256 B per slot by 32 lanes x 8 B
+    const uint32_t f = t >> 5, q = t & 31u;
+    if (f >= n) return;
+    const uint2 v = *reinterpret_cast<const uint2*>(slots + (size_t)f * cap + 8u * q);
+    if ((v.x ^ v.y) == 0x12345678u) sink[0] = t;
+  } else if (mode == 6) {  // 256 B per slot by 16 lanes x 8 B, two loads each (the rx rows' pattern)
+    const uint32_t f = t >> 4, q = t & 15u;
+    if (f >= n) return;
+    const uint2 v = *reinterpret_cast<const uint2*>(slots + (size_t)f * cap + 8u * q);
+    const uint2 w = *reinterpret_cast<const uint2*>(slots + (size_t)f * cap + 128u + 8u * q);
+    if ((v.x ^ v.y ^ w.x ^ w.y) == 0x12345678u) sink[0] = t;
+  } else {  // mode 7: 256 B per slot by 8 lanes x 32 B (two dwordx4 each)
+    const uint32_t f = t >> 3, q = t & 7u;
+    if (f >= n) return;
+    const uint4 v = *reinterpret_cast<const uint4*>(slots + (size_t)f * cap + 32u * q);
+    const uint4 w = *reinterpret_cast<const uint4*>(slots + (size_t)f * cap + 32u * q + 16u);
+    if ((v.x ^ v.y ^ w.z ^ w.w) == 0x12345678u) sink[0] = t;
   }
+}
+
+// The receive rows' schedule: each wave takes `per` consecutive slots, four at a
+// time (one 16-lane row each, 2 x 8 B per lane = 256 B per slot), `ahead` row
+// passes issued before the first is consumed.
+template <int AHEAD>
+__global__ void __launch_bounds__(1024) rows(const uint8_t* __restrict__ slots, uint32_t n, uint32_t cap, uint32_t per,
+                                             uint32_t* sink) {
+  const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
+  const uint32_t w = blockIdx.x * 16u + (threadIdx.x >> 6);
+  const uint32_t f0 = w * per;
+  uint32_t acc = 0;
+  uint2 v[AHEAD][2];
+#pragma unroll
+  for (int a = 0; a < AHEAD; ++a) {
+    const uint32_t f = f0 + 4u * a + row;
+    const uint8_t* s = slots + (size_t)(f < n ? f : 0) * cap;
+    v[a][0] = *reinterpret_cast<const uint2*>(s + 8u * p);
+    v[a][1] = *reinterpret_cast<const uint2*>(s + 128u + 8u * p);
+  }
+  for (uint32_t j = 0; 4u * j < per; j += AHEAD) {
+#pragma unroll
+    for (int a = 0; a < AHEAD; ++a) {
+      acc ^= v[a][0].x ^ v[a][0].y ^ v[a][1].x ^ v[a][1].y;
+      const uint32_t f = f0 + 4u * (j + AHEAD + a) + row;
+      const uint8_t* s = slots + (size_t)(f < n && 4u * (j + AHEAD + a) < per ? f : 0) * cap;
+      v[a][0] = *reinterpret_cast<const uint2*>(s + 8u * p);
+      v[a][1] = *reinterpret_cast<const uint2*>(s + 128u + 8u * p);
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
 }
 
 int main() {
@@ -56,9 +106,10 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  const char* names[] = {"4 B store", "4 x 2 B + 4 B stores", "16 B store", "64 B by 4 lanes", "256 B read by 16 lanes"};
-  const uint32_t lanes[] = {1, 1, 1, 4, 16};
-  for (int mode = 0; mode < 5; ++mode) {
+  const char* names[] = {"4 B store", "4 x 2 B + 4 B stores", "16 B store", "64 B by 4 lanes", "256 B read by 16 lanes x 16 B",
+                         "256 B read by 32 lanes x 8 B", "256 B read by 16 lanes x 2 x 8 B", "256 B read by 8 lanes x 2 x 16 B"};
+  const uint32_t lanes[] = {1, 1, 1, 4, 16, 32, 16, 8};
+  for (int mode = 0; mode < 8; ++mode) {
     const uint32_t threads = n * lanes[mode];
     const uint32_t grid = (threads + 255) / 256;
     float best = 1e9f;
@@ -74,6 +125,27 @@ int main() {
     printf("{\"mode\": %d, \"what\": \"%s\", \"slots\": %u, \"ms\": %.3f, \"Mslots_per_s\": %.1f}\n", mode, names[mode], n,
            best, n / best / 1e3);
     fflush(stdout);
+  }
+  // the rows' schedule: 48 slots per wave, 1 / 2 / 4 passes ahead, 65536 slots (85 workgroups) and 1 M slots
+  for (uint32_t nn : {65536u, 1048576u}) {
+    for (int ahead : {1, 2, 4}) {
+      const uint32_t per = 48, waves = (nn + per - 1) / per, grid = (waves + 15) / 16;
+      float best = 1e9f;
+      for (int rep = 0; rep < 6; ++rep) {
+        hipEventRecord(a, 0);
+        if (ahead == 1) hipLaunchKernelGGL(rows<1>, dim3(grid), dim3(1024), 0, 0, d, nn, cap, per, sink);
+        if (ahead == 2) hipLaunchKernelGGL(rows<2>, dim3(grid), dim3(1024), 0, 0, d, nn, cap, per, sink);
+        if (ahead == 4) hipLaunchKernelGGL(rows<4>, dim3(grid), dim3(1024), 0, 0, d, nn, cap, per, sink);
+        hipEventRecord(b, 0);
+        hipEventSynchronize(b);
+        float ms = 0;
+        hipEventElapsedTime(&ms, a, b);
+        if (rep > 0 && ms < best) best = ms;
+      }
+      printf("{\"rows\": true, \"slots\": %u, \"workgroups\": %u, \"ahead\": %d, \"ms\": %.3f, \"GB_per_s\": %.1f}\n", nn,
+             grid, ahead, best, nn * 256.0 / best / 1e6);
+      fflush(stdout);
+    }
   }
   if (h[1500] != 0 && *reinterpret_cast<uint32_t*>(h + 1536 + 1500) != 1u) printf("{\"check\": \"unexpected\"}\n");
   hipHostFree(h);
