@@ -884,20 +884,69 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
       fcs = ~(res[kk].x ^ dR);
     }
 
-    // ---- stores: the fields, the padding, the FCS; the length and statuses
+    // ---- stores.  A byte that lies in a staged qword the frame's loads filled
+    // (qword < min(kRvHead, QE): it holds what memory holds) is patched into
+    // the staged copy, and the row pass below stores the patched qwords with
+    // one coalesced write per frame; any other byte is stored directly
+    // (the FCS of a frame past 72 bytes: one to three naturally aligned stores).
+    const uint32_t qlim = (uint32_t)(QE < (int32_t)kRvHead ? QE : (int32_t)kRvHead);
+    uint8_t* hb = reinterpret_cast<uint8_t*>(head + kRvHead * kk);
+    uint32_t qlo = 0xFFu, qhi = 0;
+    auto patch = [&](uint32_t o, uint32_t b) -> bool {
+      const uint32_t a = o + mis;
+      if ((a >> 3) >= qlim) return false;
+      hb[a] = (uint8_t)b;
+      qlo = (a >> 3) < qlo ? (a >> 3) : qlo;
+      qhi = (a >> 3) > qhi ? (a >> 3) : qhi;
+      return true;
+    };
     if (live) {
       if (written) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (g_off[i] != 0) tx_put16(fr + g_off[i], g_new[i]);
+        for (int i = 0; i < 4; ++i) {
+          if (g_off[i] == 0) continue;
+          const uint32_t o = g_off[i], hi8 = g_new[i] >> 8, lo8 = g_new[i] & 0xFFu;
+          const bool in0 = patch(o, hi8), in1 = patch(o + 1u, lo8);
+          if (!in0 && !in1) {
+            tx_put16(fr + o, g_new[i]);
+          } else {
+            if (!in0) fr[o] = (uint8_t)hi8;
+            if (!in1) fr[o + 1u] = (uint8_t)lo8;
+          }
+        }
       }
       if (app) {
-        for (uint32_t o = L; o < Lp; ++o) fr[o] = 0;  // runts: zero padding to 60 bytes
-        tx_put32(fr + Lp, fcs);
+        if (((L + mis) >> 3) >= qlim) {
+          for (uint32_t o = L; o < Lp; ++o) fr[o] = 0;  // runts: zero padding to 60 bytes
+          tx_put32(fr + Lp, fcs);
+        } else {  // (short frames: padding and FCS partly in the staged qwords)
+          for (uint32_t o = L; o < Lp + 4u; ++o) {
+            const uint32_t b = o < Lp ? 0u : (fcs >> (8u * (o - Lp))) & 0xFFu;
+            if (!patch(o, b)) fr[o] = (uint8_t)b;
+          }
+        }
       }
       len[fk] = app ? Lp + 4u : L;
       st_ck[fk] = (uint8_t)v;
       st_ap[fk] = (uint8_t)(FCS && !app ? 6u : 0u);
+    }
+    if (lane < kRvGroup) res[kk].y = live && qlo <= qhi ? (qlo | (qhi << 8) | 0x10000u) : 0u;
+    __builtin_amdgcn_wave_barrier();
+    // ---- the patched staged qwords [qlo, qhi] of each frame, one row per frame
+    {
+      const uint32_t p = lane & 15u, row = lane >> 4;
+      for (uint32_t j = 0; 4u * j < nrow; ++j) {
+        const uint32_t k = 4u * j + row;
+        const uint32_t sp = res[k].y;
+        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
+        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
+        uint8_t* frk = bytes + (((uint64_t)shi << 32) | slo);
+        uint2* bk = reinterpret_cast<uint2*>(frk - (reinterpret_cast<uintptr_t>(frk) & 7u));
+        if ((sp & 0x10000u) && p >= (sp & 0xFFu) && p <= ((sp >> 8) & 0xFFu)) {
+          const uint2 q = head[kRvHead * k + p];
+          *(__attribute__((address_space(1))) uint64_t*)(bk + p) = (uint64_t)q.x | ((uint64_t)q.y << 32);
+        }
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
