@@ -82,8 +82,27 @@ def main():
                        "method": "rocprofv3 --pmc FETCH_SIZE, own pass; x factor measured on tools/prof/calib "
                                  "(dword-per-lane reads of 2 GiB) in the same profiling run"}, fh, indent=1)
     c = summary["counters"]
-    if "GRBM_GUI_ACTIVE" in c and summary["avg_ns"]:
-        summary["clock_ghz_est"] = c["GRBM_GUI_ACTIVE"] / 8 / summary["avg_ns"]
+    # the clock: GRBM_GUI_ACTIVE (cycles, summed over the 8 XCDs) over the SAME
+    # dispatch's duration from the kernel trace of that pass (profile.sh traces
+    # the GRBM pass); dividing by the other pass's durations mixed an un-warmed
+    # PMC run with a warmed trace and read low (round 4's "1.9 GHz", profiles/r5l)
+    clk = []
+    for i in range(1, 10):
+        cp = os.path.join(src, f"pmc{i}", "pmc_counter_collection.csv")
+        kp = os.path.join(src, f"pmc{i}", "pmc_kernel_trace.csv")
+        if not (os.path.exists(cp) and os.path.exists(kp)):
+            continue
+        dur = {r["Dispatch_Id"]: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+               for r in csv.DictReader(open(kp)) if KERNEL in r["Kernel_Name"]}
+        grbm = collections.defaultdict(float)
+        for r in csv.DictReader(open(cp)):
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                grbm[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        clk += [grbm[d] / 8 / dur[d] for d in grbm if dur.get(d)]
+    if clk:
+        summary["clock_ghz"] = sorted(clk)[len(clk) // 2]
+        summary["clock_method"] = "median over dispatches of GRBM_GUI_ACTIVE / 8 XCDs / the dispatch's traced duration"
+    summary["clock_ghz_est"] = summary.get("clock_ghz")
     keys = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT")
     if all(k in c for k in keys):  # read by bench.py (roofline_compute): tied to the build that made them
         with open(os.path.join(dst, f"counters_{wl}.json"), "w") as fh:
