@@ -325,8 +325,10 @@ int lnx_rx_ring_stats(lnx_rx_ring* ring, lnx_rx_ring_counters* out);
 /* Zero copy (on by default): the ring's slots are mapped into the GPU's
  * address space and the kernels read the frames in place over PCIe, so no host
  * thread copies a frame and only frame bytes cross the link.  This covers
- * lnx_rx_ring_ingress and, when every buffer of a batch lies in the ring's slot
- * memory (netdev RunnerConfig.Buffers carved from lnx_rx_ring_slots,
+ * lnx_rx_ring_ingress (a batch whose frames fill >= 90 % of their slots still
+ * goes up by DMA of whole slots, the faster mover there) and, when every
+ * buffer of a batch lies in the ring's slot memory (netdev
+ * RunnerConfig.Buffers carved from lnx_rx_ring_slots,
  * x/netdev/runner.go:92-94), lnx_ingress_packets and lnx_egress_packets (whose
  * kernel then patches the frames in place: one read of each frame, stores of
  * the fields, padding and FCS only).  Other buffers are gathered into pinned

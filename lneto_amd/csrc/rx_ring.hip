@@ -448,15 +448,19 @@ int lnx_rx_ring_ingress(lnx_rx_ring* r, uint32_t first, uint32_t count, uint32_t
       const uint32_t l = std::min(r->h_len[b0 + j], r->cap);
       return l > offset ? l - offset : 0u;
     };
-    if (r->zero_copy) {  // frames read in place: no host copy, only frame bytes cross PCIe
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < nb; ++j) total += flen(j);
+    // whole slots by DMA when the frames fill them (the copy engine moves full
+    // slots faster than the kernel reads them in place: 50.9 against 42.1 GiB/s
+    // at 1500 B); else, with zero copy, the frames are read in place (only
+    // their bytes cross PCIe), without it packed on the host
+    const bool dense = total * 10 >= (uint64_t)nb * r->cap * 9;
+    if (r->zero_copy && !dense) {
       rc = enqueue_rx(r, s, nb, RxSrc::kSlotsDirect, b0, offset, flags, r->h_ok + b0, r->h_verdict + b0);
       if (rc == LNX_OK) r->stats.zero_copy_frames += nb;
       continue;
     }
-    uint64_t total = 0;
-    for (uint32_t j = 0; j < nb; ++j) total += flen(j);
-    // whole slots when the frames fill them (no host copy); else frames packed
-    const bool pack = total * 10 < (uint64_t)nb * r->cap * 9;
+    const bool pack = !dense;
     if (pack) {
       if (packed_pending[k % r->depth] && (e = hipStreamSynchronize(s.s)) != hipSuccess) {
         rc = hip_error(e, "rx ring hipStreamSynchronize");
