@@ -27,8 +27,10 @@ i=0
 for CNT in "FETCH_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY WRITE_SIZE"; do
   i=$((i+1))
   echo "[prof] pmc pass $i: $CNT"
-  # (--kernel-trace beside the counters: the GRBM pass's per-dispatch clock, summarize.py)
-  timeout -s KILL 120 rocprofv3 --pmc $CNT --kernel-trace -d $OUT/pmc$i -o pmc --output-format csv -- python3 $B --steps 5 --warmup 1 > $OUT/bench_pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
+  # (--kernel-trace beside the counters: the GRBM pass's per-dispatch clock,
+  # summarize.py; that pass warms the GPU first so its clock is the steady one)
+  BP="$B"; case "$CNT" in *GRBM*) BP="${B/--prewarm-s 0/--prewarm-s 0.5}";; esac
+  timeout -s KILL 120 rocprofv3 --pmc $CNT --kernel-trace -d $OUT/pmc$i -o pmc --output-format csv -- python3 $BP --steps 5 --warmup 1 > $OUT/bench_pmc$i.log 2>&1 || { echo "pmc pass $i failed rc=$?"; exit 1; }
 done
 echo "[prof] calibration"
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE -d $OUT/calib -o calib --output-format csv -- tools/prof/calib > $OUT/calib.log 2>&1 || { echo "calib failed rc=$?"; exit 1; }

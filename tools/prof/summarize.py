@@ -98,7 +98,8 @@ def main():
         for r in csv.DictReader(open(cp)):
             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
                 grbm[r["Dispatch_Id"]] += float(r["Counter_Value"])
-        clk += [grbm[d] / 8 / dur[d] for d in grbm if dur.get(d)]
+        ds = sorted((d for d in grbm if dur.get(d)), key=int)[-10:]  # the last, warmed dispatches
+        clk += [grbm[d] / 8 / dur[d] for d in ds]
     if clk:
         summary["clock_ghz"] = sorted(clk)[len(clk) // 2]
         summary["clock_method"] = "median over dispatches of GRBM_GUI_ACTIVE / 8 XCDs / the dispatch's traced duration"
