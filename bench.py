@@ -8,7 +8,8 @@ lnx_crc32_batch call over the rank's whole frame batch (inputs already in HBM).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--op OP]
 
 --op crc32 (default, the BASELINE metric) | fcs_append (lnx_fcs_append_batch: TX FCS
-append in place on 1496-B frames in 1536-B ring slots, lengths reset each step) | fcs_verify (lnx_fcs_verify_batch,
+append in place on 1496-B frames in 1536-B ring slots, lengths reset each step) | tx_finish (lnx_tx_finish_batch:
+checksum generate + pad + FCS of the same UDP/IPv4 frames in one read) | fcs_verify (lnx_fcs_verify_batch,
 residue check of the same frames) | sum16 (lnx_sum16_batch: RFC 791 checksum of
 every frame as one segment, random pseudo-header seeds) | ingress
 (lnx_ingress_verify_batch: the frames get Ethernet/IPv4/UDP headers written in
@@ -394,7 +395,7 @@ def main():
     ap.add_argument("--workload", default="auto",
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32",
-                    choices=["crc32", "fcs_verify", "fcs_append", "sum16", "ingress", "rx_ring", "search",
+                    choices=["crc32", "fcs_verify", "fcs_append", "tx_finish", "sum16", "ingress", "rx_ring", "search",
                              "tx_checksum", "egress_packets", "ingress_packets", "rx_verify"])
     ap.add_argument("--short-frames", action="store_true",
                     help="--op crc32 / fcs_verify through lnx_*_batch_ex(LNX_BATCH_SHORT_FRAMES): the staged "
@@ -483,6 +484,27 @@ def main():
         d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
     elif args.op == "fcs_verify":
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    elif args.op == "tx_finish":
+        # the transmit tail in one read (lnx_tx_finish_batch): UDP/IPv4 frames of
+        # flen - 4 bytes in CAP-byte slots get their length fields and checksums
+        # (idempotent) and their LE FCS in place; the lengths are restored first
+        # every step (a 4-byte-per-frame device copy, timed)
+        if flen is None:
+            raise SystemExit("--op tx_finish needs fixed-size frames")
+        cap = 1536
+        n_slots = n_local
+        d_bytes = synth.bytes_torch(n_slots * cap, dev, seed=synth.SEED + lo * 0x10001)
+        fr = d_bytes.view(n_slots, cap)
+        hdr = bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0]) + (flen - 18).to_bytes(2, "big") \
+            + bytes.fromhex("12344000401100 00c0a80a01c0a80a02".replace(" ", "")) \
+            + bytes.fromhex("14e90035") + (flen - 38).to_bytes(2, "big")
+        fr[:, : len(hdr)] = torch.tensor(list(hdr), dtype=torch.uint8, device=dev)
+        nbytes = n_slots * (flen - 4)
+        d_start = torch.arange(n_slots, dtype=torch.int64, device=dev) * cap
+        d_len0 = torch.full((n_slots,), flen - 4, dtype=torch.int32, device=dev)
+        d_len = d_len0.clone()
+        d_status = torch.empty(n_slots, dtype=torch.uint8, device=dev)
+        off_np = (np.arange(n_slots + 1, dtype=np.int64) * cap)
     elif args.op == "fcs_append":
         # TX path (internet/stack-ethernet.go:200-214): frames of flen - 4 bytes
         # in slots of CAP bytes get their LE FCS appended in place; the step
@@ -550,6 +572,10 @@ def main():
             with torch.cuda.stream(stream):
                 d_len.copy_(d_len0, non_blocking=True)
             L.fcs_append_batch(d_bytes, d_start, d_len, 1536, status=d_status, stream=stream)
+        elif args.op == "tx_finish":
+            with torch.cuda.stream(stream):
+                d_len.copy_(d_len0, non_blocking=True)
+            L.tx_finish_batch(d_bytes, d_start, d_len, 1536, flags=3, status=d_status, stream=stream)
         else:
             L.crc32_batch(d_bytes, d_off, out=d_crc, stream=stream, short_frames=args.short_frames)
 
@@ -618,6 +644,7 @@ def main():
         "rx_verify": "GiB/s receive check in one pass (FCS residue + IPv4 header / UDP verdicts) over device-resident frames",
         "search": "GiB/s CRC32Search over device-resident captures (bytes scanned to the FCS hit)",
         "fcs_append": "GiB/s TX FCS append (pad, CRC-32, LE32 store) over device-resident ring slots",
+        "tx_finish": "GiB/s transmit tail in one read (checksum generate + pad + FCS) over device-resident ring slots",
         "tx_checksum": "GiB/s TX checksum generate (IPv4 header + UDP) over device-resident frames",
     }[args.op]
     out = {
@@ -661,6 +688,7 @@ def main():
                        "rx_verify": "lnx::rx_verify_kernel<true, false>",
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
+                       "tx_finish": "lnx::tx_finish_kernel<FCS, CK, HBM>",
                        "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_window": f"HIP events around all {args.steps} timed steps on the launch stream, / {args.steps}",
@@ -727,17 +755,20 @@ def main():
             got = d_ok.cpu().numpy().astype(np.uint32) * 256 + d_verdict.cpu().numpy()
         elif args.op == "search":
             got = d_hit.cpu().numpy()
-        elif args.op == "fcs_append":
+        elif args.op in ("fcs_append", "tx_finish"):
             got = d_status.cpu().numpy()
             lens_after = d_len.cpu().numpy()
         else:
             got = d_crc.cpu().numpy().view(np.uint32)
         for i in idx:
             s, e = int(off_np[i]), int(off_np[i + 1])
-            if args.op == "fcs_append":
+            if args.op in ("fcs_append", "tx_finish"):
                 fr = d_bytes[s:s + flen].cpu().numpy().tobytes()
                 assert int(got[i]) == 0 and int(lens_after[i]) == flen, f"frame {i}: status / length"
                 assert O.crc32(fr[:-4]) == int.from_bytes(fr[-4:], "little"), f"mismatch frame {i}"
+                if args.op == "tx_finish":  # the finished frame is a fixed point of both steps and is accepted
+                    regen, st = O.tx_checksum(fr[:-4])
+                    assert st == 0 and regen == fr[:-4] and O.ingress_verdict(fr[:-4]) == 0, f"frame {i}"
                 continue
             fr = d_bytes[s:e].cpu().numpy().tobytes()
             if args.op == "sum16":
@@ -780,7 +811,8 @@ def main():
         out["pcie_inclusive"] = {"value": round(nbytes / el / 2**30, 2), "unit": "GiB/s",
                                  "note": "pinned H2D of frames + kernel + D2H of CRCs, serial, 1 stream"}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op not in ("fcs_append", "tx_checksum"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op not in ("fcs_append", "tx_checksum",
+                                                                                  "tx_finish"):
         out["cpu_baseline"] = cpu_baseline(d_bytes, off_np, flen, budget_s=args.cpu_budget, op=args.op)
 
     if rank == 0:

@@ -171,6 +171,21 @@ int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_
 int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                           uint8_t* d_status, void* stream);
 
+/* The transmit tail in ONE read of each frame: lnx_tx_checksum_batch's
+ * checksum step (flags & LNX_TX_CHECKSUM) followed by lnx_fcs_append_batch's
+ * padding and FCS (flags & LNX_TX_FCS), over the frames as the stack wrote them
+ * (StackEthernet.Encapsulate after encapsulate4 / encapsulate6,
+ * internet/stack-ethernet.go:200-214, internet/stack-ip4.go:202-228,
+ * internet/stack-ip6.go:167-181).  The CRC is taken over the frame as loaded
+ * and corrected for the fields the checksum step writes, so
+ * the result equals the two calls in sequence.  d_len[i] is updated; each frame
+ * may grow to `capacity` bytes; d_status[i] = the checksum step's status if
+ * non-zero (18, 15), else the append's (0, or 6 lneto.ErrShortBuffer with the
+ * frame left unpadded).  Frames must not overlap (any order).  The flag values
+ * are LNX_TX_CHECKSUM and LNX_TX_FCS (declared with lnx_egress_packets). */
+int lnx_tx_finish_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
+                        uint32_t flags, uint8_t* d_status, void* stream);
+
 /* FCS verify of received frames that still carry their 4-byte LE FCS:
  * d_ok[i] = 1 iff len_i >= 4 and CRC32(f[:len_i-4]) == LE32(f[len_i-4:]),
  * evaluated as the residue test CRC32(f) == LNX_CRC32_RESIDUE.  This is the

@@ -137,6 +137,7 @@ _sig = {
     "lnx_rx_ring_set_host_threshold": (ctypes.c_int, [_vp, ctypes.c_uint32]),
     "lnx_rx_ring_stats": (ctypes.c_int, [_vp, _vp]),
     "lnx_rx_ring_set_zero_copy": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "lnx_tx_finish_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     "lnx_device_count": (ctypes.c_int, []),
     "lnx_last_error": (ctypes.c_char_p, []),
     "lnx_version": (ctypes.c_char_p, []),
@@ -397,6 +398,25 @@ def tx_checksum_batch(d_bytes, d_start, d_len, status=None, stream=None):
         with b as s:
             _check(lib.lnx_tx_checksum_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n,
                                              status.data_ptr(), s), what)
+    return status
+
+
+def tx_finish_batch(d_bytes, d_start, d_len, capacity: int, flags: int = 3, status=None, stream=None):
+    """The transmit tail in one read (lnx_tx_finish_batch): the checksum step
+    (flags & TX_CHECKSUM) then padding + FCS (flags & TX_FCS) of every frame
+    d_bytes[d_start[i] : d_start[i] + d_len[i]], in place; d_len (int32) is
+    updated.  Returns the uint8 status (the checksum step's if non-zero, else
+    the append's)."""
+    import torch
+    what = "lnx_tx_finish_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_start", d_start, "i64"), ("d_len", d_len, "i32")], stream)
+    n = d_start.numel()
+    _need_len(what, "d_len", d_len, n)
+    status = _out(what, status, n, torch.uint8, "u8", b.device)
+    if n > 0:
+        with b as s:
+            _check(lib.lnx_tx_finish_batch(d_bytes.data_ptr(), d_start.data_ptr(), d_len.data_ptr(), n, capacity,
+                                           flags, status.data_ptr(), s), what)
     return status
 
 

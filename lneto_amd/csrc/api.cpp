@@ -46,6 +46,9 @@ hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* le
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
+hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
+                            uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
+                            hipStream_t stream, bool host);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream, int var = 0);
@@ -552,6 +555,20 @@ int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint3
   if (st != LNX_OK) return st;
   hipError_t e = launch_tx_checksum(d_bytes, d_start, d_len, n, d_status, c->num_cus, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "tx checksum (ingress_verify_kernel<GEN>) launch");
+  return LNX_OK;
+}
+
+int lnx_tx_finish_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
+                        uint32_t flags, uint8_t* d_status, void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_start || !d_len || !d_status) return LNX_EINVAL;
+  if ((flags & ~(uint32_t)(LNX_TX_CHECKSUM | LNX_TX_FCS)) != 0) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  const hipError_t e = launch_tx_finish(d_bytes, d_start, d_len, n, capacity, flags, d_status, d_status, c->d_rx,
+                                        c->num_cus, static_cast<hipStream_t>(stream), false);
+  if (e != hipSuccess) return hip_fail(e, "tx_finish_kernel launch");
   return LNX_OK;
 }
 

@@ -74,7 +74,7 @@ hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* le
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
-                            hipStream_t stream);
+                            hipStream_t stream, bool host);
 
 // Slot i of the batch: frame = slot[offset : min(len, cap)].
 __global__ void __launch_bounds__(256)
@@ -291,7 +291,7 @@ int enqueue_tx(lnx_rx_ring* r, Stage& s, uint32_t nb, uint64_t total, uint32_t c
     // frames in the pinned slots: one kernel reads each frame once over PCIe and
     // stores only the fields, the padding and the FCS (rx_verify_kernel.hip tx_finish)
     if ((e = launch_tx_finish(bytes, s.d_start, s.d_len, nb, capacity, flags, s.d_verdict, s.d_ok,
-                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s)) != hipSuccess)
+                              static_cast<const uint32_t*>(r->rx_image), r->num_cus, s.s, true)) != hipSuccess)
       return hip_error(e, "tx ring tx_finish launch");
   } else {
     if ((e = hipMemsetAsync(s.d_verdict, 0, nb, s.s)) != hipSuccess ||

@@ -29,7 +29,10 @@ namespace lnx {
 
 namespace {
 
-constexpr int kRvBlock = 1024;
+#ifndef LNX_RV_BLOCK
+#define LNX_RV_BLOCK 1024
+#endif
+constexpr int kRvBlock = LNX_RV_BLOCK;
 constexpr int kRvUnroll = 12;  // qwords per lane per batch (1536 bytes per row, as the ingress kernel)
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
@@ -365,7 +368,8 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
     const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
     const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
-    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+    const uint32_t nrow = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup));  // (wave-uniform passes)
 
     // ---------------------------------------------------------------- A: data
     rv_rows<CRC, false, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
@@ -679,7 +683,7 @@ __device__ __forceinline__ void tx_put32(uint8_t* q, uint32_t w) {
   }
 }
 
-template <bool FCS, bool CK>
+template <bool FCS, bool CK, bool HOST>
 __global__ void __launch_bounds__(kRvBlock)
 tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
                  uint64_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
@@ -715,8 +719,11 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint64_t fi = live ? fk : n - 1u;
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
-    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
-    rv_rows<FCS, true, true>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);  // (the ring's slots)
+    // (readfirstlane: the passes' trip count must stay wave-uniform, or hipcc
+    // makes the loops below exec-narrowing ones with 64-bit loads inside)
+    const uint32_t nrow = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup));
+    rv_rows<FCS, true, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
     __builtin_amdgcn_wave_barrier();
 
     // ---------------------------------------------------------------- B: one lane per frame
@@ -927,8 +934,13 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
         }
       }
       len[fk] = app ? Lp + 4u : L;
-      st_ck[fk] = (uint8_t)v;
-      st_ap[fk] = (uint8_t)(FCS && !app ? 6u : 0u);
+      const uint32_t ap = FCS && !app ? 6u : 0u;
+      if (st_ap == st_ck) {  // one status array: the checksum step's if non-zero, else the append's
+        st_ck[fk] = (uint8_t)(v ? v : ap);
+      } else {
+        st_ck[fk] = (uint8_t)v;
+        st_ap[fk] = (uint8_t)ap;
+      }
     }
     if (lane < kRvGroup) res[kk].y = live && qlo <= qhi ? (qlo | (qhi << 8) | 0x10000u) : 0u;
     __builtin_amdgcn_wave_barrier();
@@ -938,9 +950,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
       for (uint32_t j = 0; 4u * j < nrow; ++j) {
         const uint32_t k = 4u * j + row;
         const uint32_t sp = res[k].y;
-        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
-        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
-        uint8_t* frk = bytes + (((uint64_t)shi << 32) | slo);
+        uint8_t* frk = bytes + start[g * kRvGroup + (k < nrow ? k : 0u)];  // (row-uniform: a cache hit)
         uint2* bk = reinterpret_cast<uint2*>(frk - (reinterpret_cast<uintptr_t>(frk) & 7u));
         if ((sp & 0x10000u) && p >= (sp & 0xFFu) && p <= ((sp >> 8) & 0xFFu)) {
           const uint2 q = head[kRvHead * k + p];
@@ -954,18 +964,26 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
 
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
-                            hipStream_t stream) {
+                            hipStream_t stream, bool host) {
   if (n == 0) return hipSuccess;
   uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const bool ck = flags & 1u, fcs = flags & 2u;
-#define LNX_TX(A, C)                                                                                               \
-  hipLaunchKernelGGL((tx_finish_kernel<A, C>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, start, len, n, \
-                     capacity, st_ck, st_ap, image)
-  if (fcs) {
-    if (ck) LNX_TX(true, true); else LNX_TX(true, false);
+#define LNX_TX(A, C, H)                                                                                               \
+  hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, start, len, \
+                     n, capacity, st_ck, st_ap, image)
+  if (host) {
+    if (fcs) {
+      if (ck) LNX_TX(true, true, true); else LNX_TX(true, false, true);
+    } else {
+      if (ck) LNX_TX(false, true, true); else LNX_TX(false, false, true);
+    }
   } else {
-    if (ck) LNX_TX(false, true); else LNX_TX(false, false);
+    if (fcs) {
+      if (ck) LNX_TX(true, true, false); else LNX_TX(true, false, false);
+    } else {
+      if (ck) LNX_TX(false, true, false); else LNX_TX(false, false, false);
+    }
   }
 #undef LNX_TX
   return hipGetLastError();
