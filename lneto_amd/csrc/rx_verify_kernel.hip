@@ -29,10 +29,15 @@ namespace lnx {
 
 namespace {
 
-#ifndef LNX_RV_BLOCK
-#define LNX_RV_BLOCK 1024
+#ifndef LNX_TX_BLOCK
+#define LNX_TX_BLOCK 768
 #endif
-constexpr int kRvBlock = LNX_RV_BLOCK;
+constexpr int kRvBlock = 1024;
+// the transmit kernel wants more registers than 16 waves of 128 VGPRs give it:
+// there hipcc spills 120-130 bytes per lane to scratch, inside the row passes
+// (memory traffic 1.57 x the frame bytes, 0.71 ms on 1 M x 1500 B); 12 waves of
+// 168 VGPRs spill nothing (1.035 x, 0.48 ms; profiles/r5v_*)
+constexpr int kTxBlock = LNX_TX_BLOCK;
 constexpr int kRvUnroll = 12;  // qwords per lane per batch (1536 bytes per row, as the ingress kernel)
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
@@ -58,15 +63,17 @@ __device__ __forceinline__ uint32_t rv_ld32(const uint32_t* p) {
 __device__ __forceinline__ uint32_t rv_lds(const char* lds, uint32_t a) {
   return *reinterpret_cast<const uint32_t*>(lds + a);
 }
+// the lane's table columns: T_k's entry for byte e of the chunk at e << 8 | k << 5 | c << 2
+// (k rotated by the lane's 8-lane group, c its lane in the group); T_{4+k} is 128 bytes on
+// (an address bit below e's: the lookup's immediate offset, no registers of its own)
 struct RvLane {
-  uint32_t base[8], sel[4];
+  uint32_t base[4], sel[4];
   __device__ explicit RvLane(uint32_t lane) {
     const uint32_t g = (lane >> 3) & 3u, c = lane & 7u;
 #pragma unroll
     for (uint32_t i = 0; i < 4; ++i) {
       const uint32_t k = (i + g) & 3u;
       base[i] = (k << 5) | (c << 2);
-      base[4 + i] = ((4u + k) << 5) | (c << 2);
       sel[i] = 0x0c020400u + (k << 8);
     }
   }
@@ -75,7 +82,7 @@ struct RvLane {
 __device__ __forceinline__ uint32_t rv_unit(const char* lds, uint32_t v0, uint32_t v1, const RvLane& z) {
   uint32_t y[8];
 #pragma unroll
-  for (uint32_t i = 0; i < 4; ++i) y[4 + i] = rv_lds(lds, kRvT + __builtin_amdgcn_perm(v1, z.base[4 + i], z.sel[i]));
+  for (uint32_t i = 0; i < 4; ++i) y[4 + i] = rv_lds(lds, kRvT + 128u + __builtin_amdgcn_perm(v1, z.base[i], z.sel[i]));
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) y[i] = rv_lds(lds, kRvT + __builtin_amdgcn_perm(v0, z.base[i], z.sel[i]));
   const uint32_t t = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(y[4], y[5], y[6], 0x96), y[7], y[0], 0x96);
@@ -368,8 +375,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
     const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
     const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
-    const uint32_t nrow = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup));  // (wave-uniform passes)
+    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
 
     // ---------------------------------------------------------------- A: data
     rv_rows<CRC, false, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
@@ -658,6 +664,21 @@ __device__ __forceinline__ uint32_t tx_zk(const char* lds, uint32_t k, uint32_t 
   }
   return x;
 }
+// XOR_f Z_{k_f}(x_f) over four fields: the four chains side by side (each step
+// that some lane of the wave needs for some field maps all four)
+__device__ __forceinline__ uint32_t tx_zk4(const char* lds, const uint32_t (&k)[4], uint32_t (&x)[4]) {
+  const uint32_t ka = k[0] | k[1] | k[2] | k[3];
+#pragma unroll 1
+  for (uint32_t m = 0; m < 16u; ++m) {
+    if (__builtin_amdgcn_ballot_w64((ka >> m) & 1u) == 0) continue;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const uint32_t y = rv_nib(lds, kTxP + 512u * m, x[f]);
+      x[f] = (k[f] >> m) & 1u ? y : x[f];
+    }
+  }
+  return x[0] ^ x[1] ^ x[2] ^ x[3];
+}
 
 // store the big-endian 16-bit value v at frame address q (2 bytes)
 __device__ __forceinline__ void tx_put16(uint8_t* q, uint32_t v) {
@@ -684,27 +705,27 @@ __device__ __forceinline__ void tx_put32(uint8_t* q, uint32_t w) {
 }
 
 template <bool FCS, bool CK, bool HOST>
-__global__ void __launch_bounds__(kRvBlock)
+__global__ void __launch_bounds__(kTxBlock)
 tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
-                 uint64_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
+                 uint32_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
                  const uint32_t* __restrict__ image) {
   constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
   constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
-  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
+  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kTxBlock / 64) * kWaveBytes];
   if constexpr (FCS) {
     const uint32_t t = threadIdx.x;
-    for (uint32_t vi = t; vi < 2048u; vi += kRvBlock) {
+    for (uint32_t vi = t; vi < 2048u; vi += kTxBlock) {
       const uint32_t v = image[vi];
       uint4* row = reinterpret_cast<uint4*>(lds + kRvT + ((vi & 255u) << 8) + ((vi >> 8) << 5));
       const uint4 v4 = {v, v, v, v};
       row[0] = v4;
       row[1] = v4;
     }
-    for (uint32_t i = t; i < 32u * 128u; i += kRvBlock)
+    for (uint32_t i = t; i < 32u * 128u; i += kTxBlock)
       reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
-    for (uint32_t i = t; i < 8u * 128u; i += kRvBlock)
+    for (uint32_t i = t; i < 8u * 128u; i += kTxBlock)
       reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
-    for (uint32_t i = t; i < 16u * 128u; i += kRvBlock) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
+    for (uint32_t i = t; i < 16u * 128u; i += kTxBlock) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
     __syncthreads();
   }
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -712,17 +733,16 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
   uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (R0, S) per frame
   uint2* head = res + kRvGroup;
   const uint2* zero = g_rv_zero;
-  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
-  for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
-    const uint64_t fk = g * kRvGroup + lane;
+  // (32-bit frame indices: the launcher splits larger batches; 64-bit ones cost
+  // the kernel 30 registers' worth of scratch spills)
+  const uint32_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  for (uint32_t g = blockIdx.x * (kTxBlock / 64) + wv; g < ngroups; g += gridDim.x * (kTxBlock / 64)) {
+    const uint32_t fk = g * kRvGroup + lane;
     const bool live = lane < kRvGroup && fk < n;
-    const uint64_t fi = live ? fk : n - 1u;
+    const uint32_t fi = live ? fk : n - 1u;
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
-    // (readfirstlane: the passes' trip count must stay wave-uniform, or hipcc
-    // makes the loops below exec-narrowing ones with 64-bit loads inside)
-    const uint32_t nrow = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup));
+    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
     rv_rows<FCS, true, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
     __builtin_amdgcn_wave_barrier();
 
@@ -733,26 +753,15 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((L + mis + 7u) >> 3);
     const uint32_t kk = lane < kRvGroup ? lane : 0u;
-    uint32_t dw[22];
-#pragma unroll
-    for (uint32_t i = 0; i < kRvHead; ++i) {
-      const uint2 v = head[kRvHead * kk + i];
-      dw[2 * i] = v.x;
-      dw[2 * i + 1] = v.y;
-    }
-    const uint32_t sh = mis & 3u;
-    uint32_t F[15];
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-      const uint32_t lo = mis >= 4 ? dw[k + 1] : dw[k], hi = mis >= 4 ? dw[k + 2] : dw[k + 1];
-      F[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    }
-    auto byt = [](uint32_t w, int i) -> uint32_t { return (w >> (8 * i)) & 0xFFu; };
-    auto be16 = [&](int o) -> uint32_t {
-      const uint32_t w = (o & 3) == 3 ? __builtin_amdgcn_alignbyte(F[(o >> 2) + 1], F[o >> 2], 3) : F[o >> 2];
-      const int i = (o & 3) == 3 ? 0 : (o & 3);
-      return (byt(w, i) << 8) | byt(w, i + 1);
-    };
+    // the staged window bytes, read from LDS where used (held in registers, the
+    // header words cost the kernel its occupancy: see kTxBlock); qwords 9 and 10
+    // (IPv4 options past the staged bytes) from memory below
+    const uint8_t* hbc = reinterpret_cast<const uint8_t*>(head + kRvHead * kk);
+    const uint32_t* hw = reinterpret_cast<const uint32_t*>(head + kRvHead * kk);
+    uint32_t dx[4] = {0, 0, 0, 0};
+    auto dwd = [&](int d) -> uint32_t { return d < 2 * (int)kRvHead ? hw[d] : dx[d - 2 * (int)kRvHead]; };
+    auto byt = [&](int o) -> uint32_t { return hbc[(uint32_t)o + mis]; };  // frame byte o (o + mis < 72)
+    auto be16 = [&](int o) -> uint32_t { return (byt(o) << 8) | byt(o + 1); };
     auto dyn16 = [&](uint32_t o) -> uint32_t {  // (o + 2 <= L checked by the caller)
       const uint32_t a = o + mis;
       uint32_t b0, b1;
@@ -773,7 +782,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
       uint32_t acc = 0;
 #pragma unroll
       for (int d = decltype(D0)::value; d < decltype(D1)::value; ++d)
-        acc = rv_dot2(dw[d] & rv_range(4 * d - (int32_t)mis, a, b), acc);
+        acc = rv_dot2(dwd(d) & rv_range(4 * d - (int32_t)mis, a, b), acc);
       return acc;
     };
     using I3 = std::integral_constant<int, 3>;
@@ -796,13 +805,13 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
       } else {
         const uint32_t et = be16(12);
         if (et == 0x0800) {
-          const uint32_t ihl = byt(F[3], 2) & 15u, hl = 4 * ihl;
+          const uint32_t ihl = byt(14) & 15u, hl = 4 * ihl;
           if (L < 34) v = kErrTruncatedFrame;
           else if (ihl < 5) v = kErrInvalidLengthField;
           else if (14 + hl > L) v = kErrTruncatedFrame;
           else if (L - 14 > 0xFFFFu) v = kErrInvalidLengthField;
           if (v == 0) {
-            const uint32_t tl = L - 14, nn = tl - hl, proto = byt(F[5], 3);
+            const uint32_t tl = L - 14, nn = tl - hl, proto = byt(23);
             const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 1) ? 8u : 0u;
             if (nn < need) v = kErrTruncatedFrame;
             if (v == 0) {
@@ -826,7 +835,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
             }
           }
         } else if (et == 0x86DD) {
-          const uint32_t nn = L - 54, proto = byt(F[5], 0);
+          const uint32_t nn = L - 54, proto = byt(20);
           if (L < 54) v = kErrTruncatedFrame;
           else if (nn > 0xFFFFu) v = kErrInvalidLengthField;
           const uint32_t need = proto == 6 ? 20u : (proto == 17 || proto == 58) ? 8u : 0u;
@@ -855,8 +864,8 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
         const int32_t q = (int32_t)kRvHead + i;
         const bool need = l4_sum && la + (int32_t)mis > 8 * (int32_t)kRvHead && q < QE;
         const uint2 v2 = rv_ld(need ? base2 + q : zero);
-        dw[2 * q] = v2.x;
-        dw[2 * q + 1] = v2.y;
+        dx[2 * i] = v2.x;
+        dx[2 * i + 1] = v2.y;
       }
       const uint2 rk = res[kk];
       auto conv = [&](uint32_t S) -> uint32_t {
@@ -880,13 +889,14 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     uint32_t fcs = 0;
     if constexpr (FCS) {
       const uint32_t c = Lp < 128u ? Lp : 128u;
-      uint32_t D = 0;
+      uint32_t kf[4], xf[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t d = written && g_off[i] != 0 ? (g_old[i] ^ g_new[i]) : 0u;
-        const uint32_t dl = ((d >> 8) & 0xFFu) | ((d & 0xFFu) << 8);  // the field's first byte low
-        D ^= tx_zk(lds, app && dl ? c - g_off[i] : 0u, dl);
+        xf[i] = ((d >> 8) & 0xFFu) | ((d & 0xFFu) << 8);  // the field's first byte low
+        kf[i] = app && xf[i] ? c - g_off[i] : 0u;
       }
+      const uint32_t D = tx_zk4(lds, kf, xf);
       const uint32_t dR = tx_zk(lds, app ? Lp - c : 0u, D);
       fcs = ~(res[kk].x ^ dR);
     }
@@ -942,17 +952,25 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
         st_ap[fk] = (uint8_t)ap;
       }
     }
-    if (lane < kRvGroup) res[kk].y = live && qlo <= qhi ? (qlo | (qhi << 8) | 0x10000u) : 0u;
+    // the frame's start (< 2^55) and the span of its patched staged qwords for the rows below
+    // (bits 23..31 of the high word: 1 | qlo << 1 | qhi << 5, or 0 when there are none)
+    if (lane < kRvGroup)
+      res[kk] = make_uint2((uint32_t)sk, (uint32_t)(sk >> 32) | ((live && qlo <= qhi ? 1u | qlo << 1 | qhi << 5 : 0u) << 23));
     __builtin_amdgcn_wave_barrier();
     // ---- the patched staged qwords [qlo, qhi] of each frame, one row per frame
     {
       const uint32_t p = lane & 15u, row = lane >> 4;
-      for (uint32_t j = 0; 4u * j < nrow; ++j) {
+      // (readfirstlane: the trip count must stay wave-uniform, or hipcc makes
+      // this an exec-narrowing loop with 64-bit loads inside; not in phase A,
+      // where it costs 130 bytes of scratch spills per lane)
+      const uint32_t nrw = (uint32_t)__builtin_amdgcn_readfirstlane((int)nrow);
+      for (uint32_t j = 0; 4u * j < nrw; ++j) {
         const uint32_t k = 4u * j + row;
-        const uint32_t sp = res[k].y;
-        uint8_t* frk = bytes + start[g * kRvGroup + (k < nrow ? k : 0u)];  // (row-uniform: a cache hit)
+        const uint2 rk = res[k];
+        const uint32_t sp = rk.y >> 23;
+        uint8_t* frk = bytes + (((uint64_t)(rk.y & 0x7FFFFFu) << 32) | rk.x);
         uint2* bk = reinterpret_cast<uint2*>(frk - (reinterpret_cast<uintptr_t>(frk) & 7u));
-        if ((sp & 0x10000u) && p >= (sp & 0xFFu) && p <= ((sp >> 8) & 0xFFu)) {
+        if ((sp & 1u) && p >= ((sp >> 1) & 15u) && p <= (sp >> 5)) {
           const uint2 q = head[kRvHead * k + p];
           *(__attribute__((address_space(1))) uint64_t*)(bk + p) = (uint64_t)q.x | ((uint64_t)q.y << 32);
         }
@@ -965,28 +983,34 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
                             hipStream_t stream, bool host) {
-  if (n == 0) return hipSuccess;
-  uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
-  if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
   const bool ck = flags & 1u, fcs = flags & 2u;
-#define LNX_TX(A, C, H)                                                                                               \
-  hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, start, len, \
-                     n, capacity, st_ck, st_ap, image)
-  if (host) {
-    if (fcs) {
-      if (ck) LNX_TX(true, true, true); else LNX_TX(true, false, true);
+  // batches of up to 2^31 frames (the kernel's 32-bit frame indices)
+  for (uint64_t f0 = 0; f0 < n; f0 += 1ull << 31) {
+    const uint32_t m = (uint32_t)(n - f0 < (1ull << 31) ? n - f0 : 1ull << 31);
+    uint64_t grid = ((uint64_t)m + (kTxBlock / 64) * kRvGroup - 1) / ((kTxBlock / 64) * kRvGroup);
+    if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+    uint8_t* sa = st_ap == st_ck ? st_ck + f0 : st_ap + f0;
+#define LNX_TX(A, C, H)                                                                                                 \
+  hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3(kTxBlock), 0, stream, bytes, start + f0, \
+                     len + f0, m, capacity, st_ck + f0, sa, image)
+    if (host) {
+      if (fcs) {
+        if (ck) LNX_TX(true, true, true); else LNX_TX(true, false, true);
+      } else {
+        if (ck) LNX_TX(false, true, true); else LNX_TX(false, false, true);
+      }
     } else {
-      if (ck) LNX_TX(false, true, true); else LNX_TX(false, false, true);
+      if (fcs) {
+        if (ck) LNX_TX(true, true, false); else LNX_TX(true, false, false);
+      } else {
+        if (ck) LNX_TX(false, true, false); else LNX_TX(false, false, false);
+      }
     }
-  } else {
-    if (fcs) {
-      if (ck) LNX_TX(true, true, false); else LNX_TX(true, false, false);
-    } else {
-      if (ck) LNX_TX(false, true, false); else LNX_TX(false, false, false);
-    }
-  }
 #undef LNX_TX
-  return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,

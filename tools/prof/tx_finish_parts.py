@@ -1,7 +1,7 @@
 """Time lnx_tx_finish_batch on 1 M x 1496-B UDP/IPv4 frames in 1536-B slots
 (bench.py --op tx_finish) by flags (3: checksum + FCS, 2: FCS only, 1:
-checksum only), the two-call sequence, and rx_verify_batch on the same bytes
-packed, by HIP events (median of 20; the length restore timed alone too)."""
+checksum only), the two-call sequence, and rx_verify_batch on random bytes
+packed and on bench.py --op rx_verify's frames, by HIP events (median of 20; the length restore timed alone too)."""
 import json
 import numpy as np
 import torch
@@ -21,6 +21,10 @@ dl = l0.clone()
 st = torch.empty(n, dtype=torch.uint8, device=dev)
 p = synth.bytes_torch(n * flen, dev)
 o = torch.arange(n + 1, dtype=torch.int64, device=dev) * flen
+ph = synth.bytes_torch(n * flen, dev)  # the same with bench.py --op rx_verify's UDP/IPv4 headers
+hdr2 = bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0]) + (flen - 14).to_bytes(2, "big") \
+    + bytes.fromhex("1234400040110000c0a80a01c0a80a02") + bytes.fromhex("14e90035") + (flen - 34).to_bytes(2, "big")
+ph.view(n, flen)[:, : len(hdr2)] = torch.tensor(list(hdr2), dtype=torch.uint8, device=dev)
 
 
 def t(fn, reps=20):
@@ -57,6 +61,7 @@ out = {
     "tx_finish_1_ms": t(fin(1)),
     "two_calls_ms": t(two),
     "rx_verify_packed_ms": t(lambda: L.rx_verify_batch(p, o)),
+    "rx_verify_headers_ms": t(lambda: L.rx_verify_batch(ph, o)),
     "rx_verify_packed_no_fcs_ms": t(lambda: L.rx_verify_batch(p, o, flags=L.RX_NO_FCS)),
 }
 print(json.dumps(out))
