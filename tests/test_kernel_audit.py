@@ -55,6 +55,14 @@ def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "prof", "audit_loops.py"), str(tmp_path / asm)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+    if build == "product":
+        # no product kernel spills to scratch: round 5's rx_verify / tx_finish
+        # spills (120-170 bytes per lane, reloaded in the row passes) doubled
+        # their memory traffic and time
+        meta = open(tmp_path / asm).read()
+        spills = re.findall(r"\.name:\s+(\S+)\s*\n(?:.*\n)*?\s+\.private_segment_fixed_size:\s+(\d+)", meta)
+        assert spills, "no kernel metadata found"
+        assert all(int(b) == 0 for _, b in spills), [(k, b) for k, b in spills if int(b)]
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
