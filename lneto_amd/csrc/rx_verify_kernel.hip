@@ -36,8 +36,15 @@ constexpr int kRvBlock = 1024;
 // the transmit kernel wants more registers than 16 waves of 128 VGPRs give it:
 // there hipcc spills 120-130 bytes per lane to scratch, inside the row passes
 // (memory traffic 1.57 x the frame bytes, 0.71 ms on 1 M x 1500 B); 12 waves of
-// 168 VGPRs spill nothing (1.035 x, 0.48 ms; profiles/r5v_*)
+// 168 VGPRs spill nothing (1.035 x, 0.48 ms; profiles/r5v_*).  Over host memory
+// (the ring's zero-copy egress, PCIe-bound) 12 and 16 waves measured alike:
+// 17.4-24.5 GiB/s on the Zipf mix, the second process of a pair faster
+// whichever it ran (tools/prof/r5w.sh, r5y.sh)
 constexpr int kTxBlock = LNX_TX_BLOCK;
+#ifndef LNX_TX_BLOCK_HOST
+#define LNX_TX_BLOCK_HOST 768
+#endif
+constexpr int kTxBlockHost = LNX_TX_BLOCK_HOST;
 constexpr int kRvUnroll = 12;  // qwords per lane per batch (1536 bytes per row, as the ingress kernel)
 constexpr uint32_t kErrPacketDrop = 2, kErrBadCRC = 3, kErrInvalidField = 14, kErrInvalidLengthField = 15,
                    kErrTruncatedFrame = 18;
@@ -705,27 +712,28 @@ __device__ __forceinline__ void tx_put32(uint8_t* q, uint32_t w) {
 }
 
 template <bool FCS, bool CK, bool HOST>
-__global__ void __launch_bounds__(kTxBlock)
+__global__ void __launch_bounds__(HOST ? kTxBlockHost : kTxBlock)
 tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
                  uint32_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
                  const uint32_t* __restrict__ image) {
+  constexpr uint32_t kB = HOST ? kTxBlockHost : kTxBlock;
   constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
   constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
-  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kTxBlock / 64) * kWaveBytes];
+  __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kB / 64) * kWaveBytes];
   if constexpr (FCS) {
     const uint32_t t = threadIdx.x;
-    for (uint32_t vi = t; vi < 2048u; vi += kTxBlock) {
+    for (uint32_t vi = t; vi < 2048u; vi += kB) {
       const uint32_t v = image[vi];
       uint4* row = reinterpret_cast<uint4*>(lds + kRvT + ((vi & 255u) << 8) + ((vi >> 8) << 5));
       const uint4 v4 = {v, v, v, v};
       row[0] = v4;
       row[1] = v4;
     }
-    for (uint32_t i = t; i < 32u * 128u; i += kTxBlock)
+    for (uint32_t i = t; i < 32u * 128u; i += kB)
       reinterpret_cast<uint32_t*>(lds + kRvF)[32u * (i & 127u) + (i >> 7)] = image[kRvImgF + i];
-    for (uint32_t i = t; i < 8u * 128u; i += kTxBlock)
+    for (uint32_t i = t; i < 8u * 128u; i += kB)
       reinterpret_cast<uint32_t*>(lds + kRvB)[i] = image[kRvImgF + 32u * 128u + i];
-    for (uint32_t i = t; i < 16u * 128u; i += kTxBlock) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
+    for (uint32_t i = t; i < 16u * 128u; i += kB) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
     __syncthreads();
   }
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -736,7 +744,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
   // (32-bit frame indices: the launcher splits larger batches; 64-bit ones cost
   // the kernel 30 registers' worth of scratch spills)
   const uint32_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
-  for (uint32_t g = blockIdx.x * (kTxBlock / 64) + wv; g < ngroups; g += gridDim.x * (kTxBlock / 64)) {
+  for (uint32_t g = blockIdx.x * (kB / 64) + wv; g < ngroups; g += gridDim.x * (kB / 64)) {
     const uint32_t fk = g * kRvGroup + lane;
     const bool live = lane < kRvGroup && fk < n;
     const uint32_t fi = live ? fk : n - 1u;
@@ -987,11 +995,12 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
   // batches of up to 2^31 frames (the kernel's 32-bit frame indices)
   for (uint64_t f0 = 0; f0 < n; f0 += 1ull << 31) {
     const uint32_t m = (uint32_t)(n - f0 < (1ull << 31) ? n - f0 : 1ull << 31);
-    uint64_t grid = ((uint64_t)m + (kTxBlock / 64) * kRvGroup - 1) / ((kTxBlock / 64) * kRvGroup);
+    const uint64_t blk = host ? kTxBlockHost : kTxBlock;
+    uint64_t grid = ((uint64_t)m + (blk / 64) * kRvGroup - 1) / ((blk / 64) * kRvGroup);
     if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
     uint8_t* sa = st_ap == st_ck ? st_ck + f0 : st_ap + f0;
 #define LNX_TX(A, C, H)                                                                                                 \
-  hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3(kTxBlock), 0, stream, bytes, start + f0, \
+  hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3((unsigned)blk), 0, stream, bytes, start + f0, \
                      len + f0, m, capacity, st_ck + f0, sa, image)
     if (host) {
       if (fcs) {
