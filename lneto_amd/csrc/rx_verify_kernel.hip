@@ -95,19 +95,28 @@ __device__ __forceinline__ uint32_t rv_unit(const char* lds, uint32_t v0, uint32
   const uint32_t t = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(y[4], y[5], y[6], 0x96), y[7], y[0], 0x96);
   return __builtin_amdgcn_bitop3_b32(t, y[1], y[2], 0x96) ^ y[3];
 }
-// a nibble-table map (table at byte address t)
+// a nibble-table map (table at byte address t, a multiple of 64).  The entry's
+// byte address is (v's nibble i, shifted into place and masked) OR the table's
+// base, one v_and_or_b32 after the shift, and the 64 i (F: 2048 i) a ds_read
+// offset: 2 VALU per nibble instead of 3
 __device__ __forceinline__ uint32_t rv_nib(const char* lds, uint32_t t, uint32_t v) {
   uint32_t a = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < 8; ++i) a ^= rv_lds(lds, t + 64u * i + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 2));
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t sh = i == 0 ? v << 2 : v >> (4 * i - 2);
+    a ^= *reinterpret_cast<const uint32_t*>(lds + ((sh & 0x3Cu) | t) + 64u * i);
+  }
   return a;
 }
 // the same for F_q in its banked layout (entry e of table q at dword 32 e + q)
 __device__ __forceinline__ uint32_t rv_nib_f(const char* lds, uint32_t q, uint32_t v) {
+  const uint32_t t = kRvF + 4u * q;  // (bits 2..6 and 16: clear of the entry's bits 7..10)
   uint32_t a = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < 8; ++i)
-    a ^= rv_lds(lds, kRvF + 4u * q + ((16u * i + __builtin_amdgcn_ubfe(v, 4 * i, 4)) << 7));
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t sh = i == 0 ? v << 7 : i == 1 ? v << 3 : v >> (4 * i - 7);
+    a ^= *reinterpret_cast<const uint32_t*>(lds + ((sh & 0x780u) | t) + 2048u * i);
+  }
   return a;
 }
 __device__ __forceinline__ uint32_t rv_row_xor(uint32_t v) {
@@ -209,16 +218,32 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
     uint2 pf[PR][PQ];
     const uint8_t* frn[PR];
     uint32_t Ltn[PR];
+    // (a unit whose qwords lie inside all four rows' frames -- the wave's least
+    // qword count says so, wave-uniformly -- loads them at the frame's address
+    // plus an immediate offset; else each lane selects its qword or the zero
+    // qword: 4 VALU per load, 40 per pass of MTU frames saved)
+    auto wave_min = [&](int32_t x) -> int32_t {
+      x = min(x, __shfl_xor(x, 16));
+      x = min(x, __shfl_xor(x, 32));
+      return __builtin_amdgcn_readfirstlane(x);
+    };
     auto prefetch = [&](int slot, uint32_t jn) {
       if (4u * jn >= nrow) return;  // (wave-uniform)
       row_frame(jn, frn[slot], Ltn[slot]);
       const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(frn[slot]) & 7u);
       const uint2* b2 = reinterpret_cast<const uint2*>(frn[slot] - m2);
       const int32_t Q2 = (int32_t)((Ltn[slot] + m2 + 7u) >> 3);
+      const int32_t qm = wave_min(Q2);
+      if (qm >= 16 * PQ) {
 #pragma unroll
-      for (int u = 0; u < PQ; ++u) {
-        const int32_t q = (int32_t)p + 16 * u;
-        pf[slot][u] = rv_ld(q < Q2 ? b2 + q : zero);
+        for (int u = 0; u < PQ; ++u) pf[slot][u] = rv_ld(b2 + (int32_t)p + 16 * u);
+        asm volatile("");  // (keeps the two arms' loads apart: merged, every load takes the select)
+      } else {
+#pragma unroll
+        for (int u = 0; u < PQ; ++u) {
+          const int32_t q = (int32_t)p + 16 * u;
+          pf[slot][u] = rv_ld(q < Q2 ? b2 + q : zero);
+        }
       }
     };
 #pragma unroll
@@ -238,9 +263,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       nit = max(nit, __shfl_xor(nit, 16));
       nit = max(nit, __shfl_xor(nit, 32));
       nit = __builtin_amdgcn_readfirstlane(nit);
-      qmin = min(qmin, __shfl_xor(qmin, 16));
-      qmin = min(qmin, __shfl_xor(qmin, 32));
-      qmin = __builtin_amdgcn_readfirstlane(qmin);
+      qmin = wave_min(qmin);
       uint32_t r = 0, S = 0;
       // the qwords holding the bytes at or past L (the FCS, the last qword's
       // bytes past the frame) went into S, those past Lt into the CRC of lines
@@ -284,10 +307,18 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
         uint2 y[kRvUnroll];
 #pragma unroll
         for (int u = 0; u < PQ; ++u) y[u] = pf[0][u];
+        if (qmin >= 16 * (kRvUnroll - 1)) {  // (MTU frames: the last unit alone may pass the frame's end)
 #pragma unroll
-        for (int u = PQ; u < kRvUnroll; ++u) {
-          const int32_t q = (int32_t)p + 16 * u;
-          y[u] = rv_ld(q < QE ? base2 + q : zero);
+          for (int u = PQ; u < kRvUnroll - 1; ++u) y[u] = rv_ld(base2 + (int32_t)p + 16 * u);
+          const int32_t q = (int32_t)p + 16 * (kRvUnroll - 1);
+          y[kRvUnroll - 1] = rv_ld(q < QE ? base2 + q : zero);
+          asm volatile("");
+        } else {
+#pragma unroll
+          for (int u = PQ; u < kRvUnroll; ++u) {
+            const int32_t q = (int32_t)p + 16 * u;
+            y[u] = rv_ld(q < QE ? base2 + q : zero);
+          }
         }
         // the prefetch slots move down one; the last takes pass j + PR
 #pragma unroll
