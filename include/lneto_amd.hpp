@@ -193,6 +193,16 @@ inline int GenerateChecksumsBatch(uint8_t* d_bytes, const uint64_t* d_start, con
   return lnx_tx_checksum_batch(d_bytes, d_start, d_len, n, d_status, stream);
 }
 
+// The transmit tail in one read of each frame (lnx_tx_finish_batch): the
+// checksum step above (flags & LNX_TX_CHECKSUM), then StackEthernet.Encapsulate's
+// padding to 60 bytes and LE FCS (flags & LNX_TX_FCS, internet/stack-ethernet.go:
+// 200-214) within `capacity` bytes of each start; d_len updated in place;
+// status: the checksum step's 18 / 15 if non-zero, else 0 or 6 (ErrShortBuffer).
+inline int FinishBatch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
+                       uint8_t* d_status, uint32_t flags = LNX_TX_CHECKSUM | LNX_TX_FCS, void* stream = nullptr) {
+  return lnx_tx_finish_batch(d_bytes, d_start, d_len, n, capacity, flags, d_status, stream);
+}
+
 // The stack configuration the receive path consults before and between its
 // checksum checks (lnx_rx_filter): the Ethernet stack's MAC and multicast
 // acceptance (internet/stack-ethernet.go:56-58,146-152), the EtherTypes with a

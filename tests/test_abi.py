@@ -52,6 +52,15 @@ def test_batch_entry_points_validate_without_gpu():
     assert L.lib.lnx_crc32_batch_ex(None, None, 5, None, L.BATCH_SHORT_FRAMES, None) == L.LNX_EINVAL
     assert L.lib.lnx_crc32_batch_ex(None, None, 0, None, 2, None) == L.LNX_EINVAL  # unknown flag bit
     assert L.lib.lnx_fcs_verify_batch_ex(None, None, 0, None, L.BATCH_SHORT_FRAMES, None) == 0
+    # the transmit tail in one read: NULL buffers, unknown flag bits
+    assert L.lib.lnx_tx_finish_batch(None, None, None, 0, 1536, 3, None, None) == 0
+    assert L.lib.lnx_tx_finish_batch(None, None, None, 5, 1536, 3, None, None) == L.LNX_EINVAL
+    b1 = (ctypes.c_uint8 * 64)()
+    s1 = (ctypes.c_uint64 * 1)(0)
+    l1 = (ctypes.c_uint32 * 1)(60)
+    st1 = (ctypes.c_uint8 * 1)()
+    assert L.lib.lnx_tx_finish_batch(ctypes.addressof(b1), ctypes.addressof(s1), ctypes.addressof(l1), 1, 64, 4,
+                                     ctypes.addressof(st1), None) == L.LNX_EINVAL
     buf = (ctypes.c_uint8 * 8)()
     off = (ctypes.c_uint64 * 2)(0, 100)  # offset beyond nbytes
     out = (ctypes.c_uint32 * 1)()
