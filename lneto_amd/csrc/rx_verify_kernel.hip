@@ -185,7 +185,11 @@ __device__ __forceinline__ uint32_t rv_dot2(uint32_t w, uint32_t acc) {
 // a group are loaded once, by the lane of each frame.
 constexpr uint32_t kRvGroup = 48;  // frames per wave and group (LDS: tables + 16 x group staging <= 160 KiB)
 constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 72 - mis) >= [0, 65)
-constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead
+constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead (transmit)
+#ifndef LNX_RV_PF_RX
+#define LNX_RV_PF_RX 12
+#endif
+constexpr int kRvPfRx = LNX_RV_PF_RX;  // ... (receive: the whole next pass)
 __device__ uint2 g_rv_zero[2];
 
 // Phase A of a group (see above): kRvGroup / 4 passes of four 16-lane rows.
@@ -199,7 +203,7 @@ __device__ uint2 g_rv_zero[2];
 // The frame's first kRvHead qwords go to head.  HOST (frames in pinned host
 // memory, read over PCIe): the qwords past the frame's end are captured as the
 // fold passes them instead of loaded again (a second PCIe round trip).
-template <bool CRC, bool TX, bool HOST>
+template <bool CRC, bool TX, bool HOST, int PF = kRvPf>
 __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head, const RvLane& z, const uint8_t* bytes,
                                         uint64_t sk, uint32_t Ltk, uint32_t nrow, uint32_t trim, uint32_t capacity) {
   const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
@@ -214,7 +218,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
     };
     // the first PQ qwords of a pass's batch 0 are loaded PR passes before
     // (software pipelining: their latency overlaps the previous frames' folds)
-    constexpr int PR = 1, PQ = kRvPf;  // (two passes ahead for host memory measured no faster: 33.8 against 35-37 GiB/s)
+    constexpr int PR = 1, PQ = PF;  // (two passes ahead for host memory measured no faster: 33.8 against 35-37 GiB/s)
     uint2 pf[PR][PQ];
     const uint8_t* frn[PR];
     uint32_t Ltn[PR];
@@ -237,7 +241,13 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       if (qm >= 16 * PQ) {
 #pragma unroll
         for (int u = 0; u < PQ; ++u) pf[slot][u] = rv_ld(b2 + (int32_t)p + 16 * u);
-        asm volatile("");  // (keeps the two arms' loads apart: merged, every load takes the select)
+        asm volatile("");  // (keeps the arms' loads apart: merged, every load takes the select)
+      } else if (qm >= 16 * (PQ - 1)) {  // (MTU frames: the last unit alone may pass the frame's end)
+#pragma unroll
+        for (int u = 0; u < PQ - 1; ++u) pf[slot][u] = rv_ld(b2 + (int32_t)p + 16 * u);
+        const int32_t q = (int32_t)p + 16 * (PQ - 1);
+        pf[slot][PQ - 1] = rv_ld(q < Q2 ? b2 + q : zero);
+        asm volatile("");
       } else {
 #pragma unroll
         for (int u = 0; u < PQ; ++u) {
@@ -307,17 +317,19 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
         uint2 y[kRvUnroll];
 #pragma unroll
         for (int u = 0; u < PQ; ++u) y[u] = pf[0][u];
-        if (qmin >= 16 * (kRvUnroll - 1)) {  // (MTU frames: the last unit alone may pass the frame's end)
+        if constexpr (PQ < kRvUnroll) {
+          if (qmin >= 16 * (kRvUnroll - 1)) {  // (MTU frames: the last unit alone may pass the frame's end)
 #pragma unroll
-          for (int u = PQ; u < kRvUnroll - 1; ++u) y[u] = rv_ld(base2 + (int32_t)p + 16 * u);
-          const int32_t q = (int32_t)p + 16 * (kRvUnroll - 1);
-          y[kRvUnroll - 1] = rv_ld(q < QE ? base2 + q : zero);
-          asm volatile("");
-        } else {
+            for (int u = PQ; u < kRvUnroll - 1; ++u) y[u] = rv_ld(base2 + (int32_t)p + 16 * u);
+            const int32_t q = (int32_t)p + 16 * (kRvUnroll - 1);
+            y[kRvUnroll - 1] = rv_ld(q < QE ? base2 + q : zero);
+            asm volatile("");
+          } else {
 #pragma unroll
-          for (int u = PQ; u < kRvUnroll; ++u) {
-            const int32_t q = (int32_t)p + 16 * u;
-            y[u] = rv_ld(q < QE ? base2 + q : zero);
+            for (int u = PQ; u < kRvUnroll; ++u) {
+              const int32_t q = (int32_t)p + 16 * u;
+              y[u] = rv_ld(q < QE ? base2 + q : zero);
+            }
           }
         }
         // the prefetch slots move down one; the last takes pass j + PR
@@ -416,7 +428,9 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
 
     // ---------------------------------------------------------------- A: data
-    rv_rows<CRC, false, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
+    // (the whole next pass loaded ahead from HBM: 0.335 against 0.340-0.344 ms for 8 of
+    // its 12 qwords; over PCIe 8 measured 34.4 against 33.7 GiB/s)
+    rv_rows<CRC, false, HOST, HOST ? kRvPf : kRvPfRx>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
     __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, read back in order below)
 
     // ---------------------------------------------------------------- B: verdicts
