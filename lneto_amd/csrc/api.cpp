@@ -790,7 +790,9 @@ const char* lnx_version(void) {
          "CRC32Search (eight captures per wave, 192-byte lane segments as four 48-byte chains joined by "
          "lane-private Z_48 nibble tables, 3-level scan, Z_4 in the lane-private U layout, pass B by word checks, "
          "group-descriptor loads) + staged lane streams for short-frame batches (slicing-by-8 fold, LDS transposed "
-         "whole-line loads)";
+         "whole-line loads) and slice dispatch on the device + rx_verify (FCS and verdicts in one read: 16-lane "
+         "rows, 48-frame groups, the next pass loaded ahead) + tx_finish (checksums, padding and FCS in one read, "
+         "CRC corrected by linearity; 12 waves) + zero copy through the ring's pinned slots";
 }
 
 }  // extern "C"
