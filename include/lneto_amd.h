@@ -133,7 +133,8 @@ int lnx_fcs_verify_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint6
 
 /* Segment form of lnx_crc32_batch for frames that are not packed back to back
  * (ring slots): d_crc[i] = CRC32(d_bytes[d_start[i] : d_start[i] + d_len[i]]).
- * Frames must be in increasing address order and must not overlap. */
+ * Frames must be in increasing address order and must not overlap (out of
+ * order: undefined behaviour, as for lnx_fcs_append_batch). */
 int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                        uint32_t* d_crc, void* stream);
 
@@ -144,8 +145,11 @@ int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const ui
  * LE32(CRC32(padded frame)) after it, d_len[i] = padded length + 4.  Each frame
  * may grow to `capacity` bytes; a frame that would not fit is left untouched
  * with d_status[i] = 6 (lneto.ErrShortBuffer), else d_status[i] = 0.  Frames in
- * increasing address order, at least `capacity` bytes apart.  The reference's
- * onSend hook (between padding and FCS) has no batch equivalent. */
+ * increasing address order, at least `capacity` bytes apart: the kernel
+ * addresses a workgroup's frames relative to its first one, so frames out of
+ * order are undefined behaviour (wrong results, or a GPU memory fault);
+ * lnx_tx_finish_batch with LNX_TX_FCS takes frames in any order.  The
+ * reference's onSend hook (between padding and FCS) has no batch equivalent. */
 int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
                          uint8_t* d_status, void* stream);
 

@@ -113,3 +113,38 @@ def test_tx_finish_mtu_round_trip(cuda):
     crc = L.crc32_segments(d, ds, seg).cpu().numpy().view(np.uint32)
     assert (crc == O.CRC32_RESIDUE).all()
     assert np.array_equal(d.cpu().numpy().reshape(n, 1536)[:, :flen], rows)
+
+
+def test_tx_finish_equals_the_two_calls_at_scale(cuda):
+    """256 Ki frames (the generated ones of every kind, tiled in random order,
+    at random leads in 2048-B slots): the same bytes, lengths and statuses as
+    lnx_tx_checksum_batch then lnx_fcs_append_batch, over 5462 groups."""
+    import torch
+    import lneto_amd as L
+    from tests.test_tx_checksum import tx_frames
+    rng = np.random.default_rng(11)
+    base = [f for f in tx_frames(seed=400, count=4400) if len(f) <= 1900]
+    n = 1 << 18
+    pick = rng.integers(0, len(base), n)
+    lead = rng.integers(0, 16, n)
+    # slots in increasing address order: lnx_fcs_append_batch's precondition
+    # (lneto_amd.h; tx_finish itself takes any order, test_tx_finish_matches_oracle)
+    buf = rng.integers(0, 256, SLOT * n + 64, dtype=np.uint8)
+    starts = (np.arange(n, dtype=np.int64) * SLOT + lead).astype(np.int64)
+    lens = np.array([len(base[i]) for i in pick], dtype=np.int32)
+    arrs = [np.frombuffer(f, np.uint8) for f in base]
+    for k in range(n):
+        s0 = int(starts[k])
+        buf[s0:s0 + int(lens[k])] = arrs[pick[k]]
+    cap = int(lens.max()) + 2  # the longest frames have no room for the FCS: status 6
+    a = torch.from_numpy(buf).to(cuda)
+    b = a.clone()
+    ds = torch.from_numpy(starts).to(cuda)
+    la, lb = torch.from_numpy(lens).to(cuda), torch.from_numpy(lens.copy()).to(cuda)
+    st = L.tx_finish_batch(a, ds, la, cap, flags=3)
+    c1 = L.tx_checksum_batch(b, ds, lb)
+    c2 = L.fcs_append_batch(b, ds, lb, cap)
+    assert torch.equal(la, lb)
+    assert torch.equal(st, torch.where(c1 != 0, c1, c2))
+    assert torch.equal(a, b)
+    assert int((st == 6).sum()) >= 1 and int((st == 0).sum()) > n // 4
