@@ -148,3 +148,30 @@ def test_tx_finish_equals_the_two_calls_at_scale(cuda):
     assert torch.equal(st, torch.where(c1 != 0, c1, c2))
     assert torch.equal(a, b)
     assert int((st == 6).sum()) >= 1 and int((st == 0).sum()) > n // 4
+
+
+@pytest.mark.parametrize("flags", [3, 2])
+def test_tx_finish_exact_fit_at_the_buffer_end(cuda, flags):
+    """Frames whose padded length + FCS is exactly their capacity, and one byte
+    more (status 6, left unpadded), each in a buffer that ends exactly where
+    its capacity does (a load or store past it would fault): lengths 0..80 and
+    MTU, the capacity from the frame's own needs."""
+    import torch
+    import lneto_amd as L
+    from tests.test_tx_checksum import tx_frames
+    rng = np.random.default_rng(21)
+    frames = [f for f in tx_frames(seed=500, count=300) if len(f) <= 1500]
+    frames += [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in (0, 1, 13, 14, 33, 59, 60, 61, 80)]
+    for f in frames:
+        want_fit, _ = _want(f, flags, 1 << 20)
+        fit = len(want_fit) if flags & 2 else len(f)
+        for cap, slack in ((fit, 0), (max(fit - 1, len(f)), 1)):
+            buf = np.zeros(cap, dtype=np.uint8)
+            buf[:len(f)] = np.frombuffer(f, np.uint8)
+            d = torch.from_numpy(buf).to(cuda)
+            ds = torch.zeros(1, dtype=torch.int64, device=cuda)
+            dl = torch.tensor([len(f)], dtype=torch.int32, device=cuda)
+            st = int(L.tx_finish_batch(d, ds, dl, cap, flags=flags).cpu()[0])
+            want, wst = _want(f, flags, cap)
+            got = d.cpu().numpy()[:int(dl.cpu()[0])].tobytes()
+            assert (got, st) == (want, wst), (len(f), cap, slack, st, wst)
