@@ -183,7 +183,12 @@ __device__ __forceinline__ uint32_t rv_dot2(uint32_t w, uint32_t acc) {
 // Every qword load reads inside the frame or a zero qword (g_rv_zero), so no
 // load crosses the frame's qwords and none is under a branch; the offsets of
 // a group are loaded once, by the lane of each frame.
-constexpr uint32_t kRvGroup = 48;  // frames per wave and group (LDS: tables + 16 x group staging <= 160 KiB)
+// frames per wave and group (LDS: tables + the waves' group staging <= 160 KiB):
+// the receive kernel's 56 (16 waves: 154 KiB) measured 0.324-0.329 ms against
+// 0.331-0.336 for 48 and 0.340 for 60; the transmit kernel's 60 (12 waves:
+// 148 KiB) 0.435 against 0.462 for 48 and 0.467 for 56 (tools/prof/r6r.sh)
+constexpr uint32_t kRvGroup = 56;
+constexpr uint32_t kTxGroup = 60;
 constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 72 - mis) >= [0, 65)
 constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead (transmit)
 #ifndef LNX_RV_PF_RX
@@ -763,7 +768,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
                  const uint32_t* __restrict__ image) {
   constexpr uint32_t kB = HOST ? kTxBlockHost : kTxBlock;
   constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
-  constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
+  constexpr uint32_t kWaveBytes = kTxGroup * 8u * (1u + kRvHead);
   __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kB / 64) * kWaveBytes];
   if constexpr (FCS) {
     const uint32_t t = threadIdx.x;
@@ -784,18 +789,18 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const RvLane z(lane);
   uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (R0, S) per frame
-  uint2* head = res + kRvGroup;
+  uint2* head = res + kTxGroup;
   const uint2* zero = g_rv_zero;
   // (32-bit frame indices: the launcher splits larger batches; 64-bit ones cost
   // the kernel 30 registers' worth of scratch spills)
-  const uint32_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  const uint32_t ngroups = (n + kTxGroup - 1u) / kTxGroup;
   for (uint32_t g = blockIdx.x * (kB / 64) + wv; g < ngroups; g += gridDim.x * (kB / 64)) {
-    const uint32_t fk = g * kRvGroup + lane;
-    const bool live = lane < kRvGroup && fk < n;
+    const uint32_t fk = g * kTxGroup + lane;
+    const bool live = lane < kTxGroup && fk < n;
     const uint32_t fi = live ? fk : n - 1u;
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
-    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+    const uint32_t nrow = (uint32_t)(n - g * kTxGroup < kTxGroup ? n - g * kTxGroup : kTxGroup);
     rv_rows<FCS, true, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
     __builtin_amdgcn_wave_barrier();
 
@@ -805,7 +810,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((L + mis + 7u) >> 3);
-    const uint32_t kk = lane < kRvGroup ? lane : 0u;
+    const uint32_t kk = lane < kTxGroup ? lane : 0u;
     // the staged window bytes, read from LDS where used (held in registers, the
     // header words cost the kernel its occupancy: see kTxBlock); qwords 9 and 10
     // (IPv4 options past the staged bytes) from memory below
@@ -1007,7 +1012,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     }
     // the frame's start (< 2^55) and the span of its patched staged qwords for the rows below
     // (bits 23..31 of the high word: 1 | qlo << 1 | qhi << 5, or 0 when there are none)
-    if (lane < kRvGroup)
+    if (lane < kTxGroup)
       res[kk] = make_uint2((uint32_t)sk, (uint32_t)(sk >> 32) | ((live && qlo <= qhi ? 1u | qlo << 1 | qhi << 5 : 0u) << 23));
     __builtin_amdgcn_wave_barrier();
     // ---- the patched staged qwords [qlo, qhi] of each frame, one row per frame
@@ -1041,7 +1046,7 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
   for (uint64_t f0 = 0; f0 < n; f0 += 1ull << 31) {
     const uint32_t m = (uint32_t)(n - f0 < (1ull << 31) ? n - f0 : 1ull << 31);
     const uint64_t blk = host ? kTxBlockHost : kTxBlock;
-    uint64_t grid = ((uint64_t)m + (blk / 64) * kRvGroup - 1) / ((blk / 64) * kRvGroup);
+    uint64_t grid = ((uint64_t)m + (blk / 64) * kTxGroup - 1) / ((blk / 64) * kTxGroup);
     if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
     uint8_t* sa = st_ap == st_ck ? st_ck + f0 : st_ap + f0;
 #define LNX_TX(A, C, H)                                                                                                 \
