@@ -183,12 +183,15 @@ __device__ __forceinline__ uint32_t rv_dot2(uint32_t w, uint32_t acc) {
 // Every qword load reads inside the frame or a zero qword (g_rv_zero), so no
 // load crosses the frame's qwords and none is under a branch; the offsets of
 // a group are loaded once, by the lane of each frame.
-// frames per wave and group (LDS: tables + the waves' group staging <= 160 KiB):
-// the receive kernel's 56 (16 waves: 154 KiB) measured 0.324-0.329 ms against
-// 0.331-0.336 for 48 and 0.340 for 60; the transmit kernel's 60 (12 waves:
-// 148 KiB) 0.435 against 0.462 for 48 and 0.467 for 56 (tools/prof/r6r.sh)
+// the most frames per wave and group (LDS: tables + the waves' group staging
+// <= 160 KiB): 56 for the receive kernel (16 waves: 154 KiB), 64 for the
+// transmit kernel (12 waves: 155 KiB); the launchers pick the size per batch
+// (balanced_group): on 1 M frames fixed sizes measured 0.331 / 0.310 / 0.322 /
+// 0.340 ms (48 / 52 / 56 / 60, receive) and 0.462 / 0.467 / 0.435 / 0.454 ms
+// (48 / 56 / 60 / 64, transmit) -- the rounds of groups times the group size
+// (tools/prof/r6r.sh, r6u.sh)
 constexpr uint32_t kRvGroup = 56;
-constexpr uint32_t kTxGroup = 60;
+constexpr uint32_t kTxGroup = 64;
 constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 72 - mis) >= [0, 65)
 constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead (transmit)
 #ifndef LNX_RV_PF_RX
@@ -393,7 +396,7 @@ template <bool CRC, bool FILT, bool HOST>
 __global__ void __launch_bounds__(kRvBlock)
 rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
                  uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
-                 const uint32_t* __restrict__ image, RxFilter filt) {
+                 const uint32_t* __restrict__ image, uint32_t gsz, RxFilter filt) {
   constexpr uint32_t kTabBytes = CRC ? kRvBytes : 0u;
   constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
   __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
@@ -420,17 +423,19 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
   uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (FCS ok, S) per frame
   uint2* head = res + kRvGroup;                                                // kRvHead qwords per frame
   const uint2* zero = g_rv_zero;
-  const uint64_t ngroups = (n + kRvGroup - 1u) / kRvGroup;
+  // gsz <= kRvGroup frames per group, a multiple of 4 (the launcher's choice:
+  // every wave gets the same number of groups, launch_rx_verify)
+  const uint64_t ngroups = (n + gsz - 1u) / gsz;
   for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
-    // the group's frames: lane k < kRvGroup holds frame g * kRvGroup + k's start and length (FCS included)
-    const uint64_t fk = g * kRvGroup + lane;
-    const bool live = lane < kRvGroup && fk < n;
+    // the group's frames: lane k < gsz holds frame g * gsz + k's start and length (FCS included)
+    const uint64_t fk = g * gsz + lane;
+    const bool live = lane < gsz && fk < n;
     const uint64_t fi = live ? fk : n - 1u;
     const uint64_t sk = off[fi];
     const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
     const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
     const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
-    const uint32_t nrow = (uint32_t)(n - g * kRvGroup < kRvGroup ? n - g * kRvGroup : kRvGroup);
+    const uint32_t nrow = (uint32_t)(n - g * gsz < gsz ? n - g * gsz : gsz);
 
     // ---------------------------------------------------------------- A: data
     // (the whole next pass loaded ahead from HBM: 0.335 against 0.340-0.344 ms for 8 of
@@ -446,7 +451,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((Lt + mis + 7u) >> 3);
-    const uint32_t kk = lane < kRvGroup ? lane : 0u;
+    const uint32_t kk = lane < gsz ? lane : 0u;
     // the staged qwords 0 .. kRvHead - 1 of the frame's window (frame offsets -mis .. 72 - mis),
     // then qwords 9, 10 from memory for the frames that need them (IPv4 options past offset 64)
     uint32_t dw[22];
@@ -765,7 +770,7 @@ template <bool FCS, bool CK, bool HOST>
 __global__ void __launch_bounds__(HOST ? kTxBlockHost : kTxBlock)
 tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
                  uint32_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
-                 const uint32_t* __restrict__ image) {
+                 const uint32_t* __restrict__ image, uint32_t gsz) {
   constexpr uint32_t kB = HOST ? kTxBlockHost : kTxBlock;
   constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
   constexpr uint32_t kWaveBytes = kTxGroup * 8u * (1u + kRvHead);
@@ -793,14 +798,15 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
   const uint2* zero = g_rv_zero;
   // (32-bit frame indices: the launcher splits larger batches; 64-bit ones cost
   // the kernel 30 registers' worth of scratch spills)
-  const uint32_t ngroups = (n + kTxGroup - 1u) / kTxGroup;
+  // gsz <= kTxGroup frames per group, a multiple of 4 (launch_tx_finish)
+  const uint32_t ngroups = (n + gsz - 1u) / gsz;
   for (uint32_t g = blockIdx.x * (kB / 64) + wv; g < ngroups; g += gridDim.x * (kB / 64)) {
-    const uint32_t fk = g * kTxGroup + lane;
-    const bool live = lane < kTxGroup && fk < n;
+    const uint32_t fk = g * gsz + lane;
+    const bool live = lane < gsz && fk < n;
     const uint32_t fi = live ? fk : n - 1u;
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
-    const uint32_t nrow = (uint32_t)(n - g * kTxGroup < kTxGroup ? n - g * kTxGroup : kTxGroup);
+    const uint32_t nrow = (uint32_t)(n - g * gsz < gsz ? n - g * gsz : gsz);
     rv_rows<FCS, true, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
     __builtin_amdgcn_wave_barrier();
 
@@ -810,7 +816,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((L + mis + 7u) >> 3);
-    const uint32_t kk = lane < kTxGroup ? lane : 0u;
+    const uint32_t kk = lane < gsz ? lane : 0u;
     // the staged window bytes, read from LDS where used (held in registers, the
     // header words cost the kernel its occupancy: see kTxBlock); qwords 9 and 10
     // (IPv4 options past the staged bytes) from memory below
@@ -1012,7 +1018,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     }
     // the frame's start (< 2^55) and the span of its patched staged qwords for the rows below
     // (bits 23..31 of the high word: 1 | qlo << 1 | qhi << 5, or 0 when there are none)
-    if (lane < kTxGroup)
+    if (lane < gsz)  // (every row pass below reads k < 4 ceil(nrow / 4) <= gsz: written this group)
       res[kk] = make_uint2((uint32_t)sk, (uint32_t)(sk >> 32) | ((live && qlo <= qhi ? 1u | qlo << 1 | qhi << 5 : 0u) << 23));
     __builtin_amdgcn_wave_barrier();
     // ---- the patched staged qwords [qlo, qhi] of each frame, one row per frame
@@ -1038,6 +1044,19 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
   }
 }
 
+// The group size for n frames over `waves` waves of at most gmax frames a
+// group: the fewest rounds of groups the waves can take (ceil(n / gmax) groups
+// over the waves), then the smallest group (a multiple of 4: the row passes)
+// that still covers n in that many rounds -- so every wave's last round is as
+// full as the others, where a fixed size left the last round 33 % (48) or
+// 57 % (56) full on 1 M frames (0.331 / 0.322 ms against 0.310 for 52)
+uint32_t balanced_group(uint64_t n, uint64_t waves, uint32_t gmax) {
+  const uint64_t rounds = ((n + gmax - 1) / gmax + waves - 1) / waves;
+  uint64_t g = (n + waves * rounds - 1) / (waves * rounds);
+  g = (g + 3) & ~3ull;
+  return (uint32_t)(g < 4 ? 4 : g > gmax ? gmax : g);
+}
+
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
                             hipStream_t stream, bool host) {
@@ -1048,10 +1067,11 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
     const uint64_t blk = host ? kTxBlockHost : kTxBlock;
     uint64_t grid = ((uint64_t)m + (blk / 64) * kTxGroup - 1) / ((blk / 64) * kTxGroup);
     if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+    const uint32_t gsz = balanced_group(m, grid * (blk / 64), kTxGroup);
     uint8_t* sa = st_ap == st_ck ? st_ck + f0 : st_ap + f0;
 #define LNX_TX(A, C, H)                                                                                                 \
   hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3((unsigned)blk), 0, stream, bytes, start + f0, \
-                     len + f0, m, capacity, st_ck + f0, sa, image)
+                     len + f0, m, capacity, st_ck + f0, sa, image, gsz)
     if (host) {
       if (fcs) {
         if (ck) LNX_TX(true, true, true); else LNX_TX(true, false, true);
@@ -1080,9 +1100,10 @@ hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t 
   if (n == 0) return hipSuccess;
   uint64_t grid = (n + (kRvBlock / 64) * kRvGroup - 1) / ((kRvBlock / 64) * kRvGroup);
   if (grid > (uint64_t)num_cus) grid = (uint64_t)num_cus;
+  const uint32_t gsz = balanced_group(n, grid * (kRvBlock / 64), kRvGroup);
 #define LNX_RV(C, F, H)                                                                                       \
   hipLaunchKernelGGL((rx_verify_kernel<C, F, H>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, off, n, \
-                     flags, ok, verdict, seg_len, image, filt)
+                     flags, ok, verdict, seg_len, image, gsz, filt)
   if (host) {
     if (fcs) {
       if (filt.on) LNX_RV(true, true, true); else LNX_RV(true, false, true);
