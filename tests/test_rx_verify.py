@@ -172,3 +172,12 @@ def _udp_rows(n, flen):
     fcs = O.crc32_frames(rows[:, :L].copy().reshape(-1), np.arange(n + 1, dtype=np.uint64) * L, threads=8)
     rows[:, L:flen] = fcs.view(np.uint8).reshape(n, 4)
     return rows
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 9, 52, 55, 57, 63, 64, 65, 897, 1000, 4097, 20000])
+def test_rx_verify_batch_sizes(cuda, n):
+    """Batches of every shape the launcher's group size takes (balanced_group:
+    4 to 56 frames a group, the last group part-full) against the oracle."""
+    base = _case_frames(G.frames(seed=70, count=400) + G.icmp_frames(seed=71, count=60), seed=72)
+    frames = [base[i % len(base)] for i in range(n)]
+    _cmp(_run(cuda, frames, n % 8), _want(frames), frames)

@@ -175,3 +175,27 @@ def test_tx_finish_exact_fit_at_the_buffer_end(cuda, flags):
             want, wst = _want(f, flags, cap)
             got = d.cpu().numpy()[:int(dl.cpu()[0])].tobytes()
             assert (got, st) == (want, wst), (len(f), cap, slack, st, wst)
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 61, 64, 65, 1000, 3073])
+def test_tx_finish_batch_sizes(cuda, n):
+    """Batches of every shape the launcher's group size takes (4 to 64 frames a
+    group, the last group part-full): the bytes, lengths and statuses of the two
+    calls."""
+    import torch
+    import lneto_amd as L
+    from tests.test_tx_checksum import tx_frames
+    rng = np.random.default_rng(n)
+    base = [f for f in tx_frames(seed=600, count=700) if len(f) <= 1500]
+    frames = [base[i % len(base)] for i in range(n)]
+    buf, starts, lens = _layout(frames, 3, np.arange(n), rng)
+    cap = 1536
+    a = torch.from_numpy(buf.copy()).to(cuda)
+    b = torch.from_numpy(buf.copy()).to(cuda)
+    ds = torch.from_numpy(starts).to(cuda)
+    la, lb = torch.from_numpy(lens.copy()).to(cuda), torch.from_numpy(lens.copy()).to(cuda)
+    st = L.tx_finish_batch(a, ds, la, cap, flags=3)
+    c1 = L.tx_checksum_batch(b, ds, lb)
+    c2 = L.fcs_append_batch(b, ds, lb, cap)
+    assert torch.equal(a, b) and torch.equal(la, lb)
+    assert torch.equal(st, torch.where(c1 != 0, c1, c2))
