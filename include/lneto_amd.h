@@ -108,24 +108,24 @@ int lnx_fcs_append(uint8_t* frame, uint32_t* len, uint32_t capacity);
  * ======================================================================== */
 
 /* d_crc[i] = CRC32(d_bytes[d_off[i] : d_off[i+1]]) for i in [0, n).
- * d_off holds n+1 non-decreasing offsets (a frame whose end offset is below
- * its start is treated as empty); frames may have any length and any byte
- * alignment.  Replaces n calls of
+ * d_off holds n+1 offsets, non-decreasing for the fast paths; offsets out of
+ * order are accepted too (a frame whose end offset is below its start is
+ * treated as empty, CRC 0; every other frame, overlapping ones included, gets
+ * the CRC of its own bytes).  Frames may have any length and any byte
+ * alignment.  Each workgroup slice's kernel is picked on the device from its
+ * offsets, so the call never reads device memory on the host
+ * and never syncs.  Replaces n calls of
  * ethernet.CRC32 (ethernet/crc.go:19-21) / of the CRC32Update hook with crc=0
  * (internet/stack-ethernet.go:211-214). */
 int lnx_crc32_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n,
                     uint32_t* d_crc, void* stream);
 
-/* lnx_crc32_batch / lnx_fcs_verify_batch with flags.  LNX_BATCH_SHORT_FRAMES:
- * the caller knows the batch's mean frame length is short (under
- * LNX_SHORT_FRAME_MEAN bytes, e.g. a receive ring holding the traffic's mix):
- * the frames are read by the staged lane-stream kernel, which requests each
- * 128-byte line once instead of per-frame windows.  Results
- * are identical either way; the flag only picks the faster kernel for the mix
- * (the library cannot see device-resident offsets without a sync).  Other
- * bits must be 0. */
+/* lnx_crc32_batch / lnx_fcs_verify_batch with flags.  LNX_BATCH_SHORT_FRAMES
+ * forces the staged lane-stream kernel (each 128-byte line
+ * requested once) for every slice that is not giant, where the plain entries
+ * let the device pick per slice (uniform lengths the rows kernel is faster at
+ * go to it).  Results are identical either way.  Other bits must be 0. */
 #define LNX_BATCH_SHORT_FRAMES 1u
-#define LNX_SHORT_FRAME_MEAN 512u
 int lnx_crc32_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t* d_crc, uint32_t flags,
                        void* stream);
 int lnx_fcs_verify_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_ok,
@@ -133,8 +133,10 @@ int lnx_fcs_verify_batch_ex(const uint8_t* d_bytes, const uint64_t* d_off, uint6
 
 /* Segment form of lnx_crc32_batch for frames that are not packed back to back
  * (ring slots): d_crc[i] = CRC32(d_bytes[d_start[i] : d_start[i] + d_len[i]]).
- * Frames must be in increasing address order and must not overlap (out of
- * order: undefined behaviour, as for lnx_fcs_append_batch). */
+ * Any order, overlap allowed.  Frames in increasing address order that do not
+ * overlap take the pipelined rows; a workgroup slice that is not
+ * (start[i] + len[i] > start[i + 1] somewhere) is folded frame by frame, each
+ * from its own start. */
 int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                        uint32_t* d_crc, void* stream);
 
@@ -144,12 +146,12 @@ int lnx_crc32_segments(const uint8_t* d_bytes, const uint64_t* d_start, const ui
  * d_bytes[d_start[i] : d_start[i] + d_len[i]]: zero-pad to 60 bytes, write
  * LE32(CRC32(padded frame)) after it, d_len[i] = padded length + 4.  Each frame
  * may grow to `capacity` bytes; a frame that would not fit is left untouched
- * with d_status[i] = 6 (lneto.ErrShortBuffer), else d_status[i] = 0.  Frames in
- * increasing address order, at least `capacity` bytes apart: the kernel
- * addresses a workgroup's frames relative to its first one, so frames out of
- * order are undefined behaviour (wrong results, or a GPU memory fault);
- * lnx_tx_finish_batch with LNX_TX_FCS takes frames in any order.  The
- * reference's onSend hook (between padding and FCS) has no batch equivalent. */
+ * with d_status[i] = 6 (lneto.ErrShortBuffer), else d_status[i] = 0.  Frames
+ * in any order; their rooms [start, start + capacity) must not overlap.  A
+ * workgroup slice in increasing address order takes the pipelined rows
+ * (addressed relative to its first frame), any other slice is folded frame by
+ * frame from each frame's own start (as lnx_crc32_segments).  The reference's
+ * onSend hook (between padding and FCS) has no batch equivalent. */
 int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_len, uint64_t n, uint32_t capacity,
                          uint8_t* d_status, void* stream);
 
@@ -398,9 +400,14 @@ int lnx_ingress_packets(lnx_rx_ring* ring, const uint8_t* const* bufs, const uin
  * packed back to back, each with room for its padding and FCS only.  On an
  * error return the frames of batches that completed before the error may
  * already be written back (with their lens and status); the failing batch's
- * and later frames, lens and status are left as they were, and every stage has
- * drained before the call returns.  lnx_ingress_packets writes results the
- * same way. */
+ * and later lens and status are left as they were, and every stage has
+ * drained before the call returns.  The failing batch's frames are left as
+ * they were too, except under zero copy (lnx_rx_ring_set_zero_copy), where the
+ * kernel patches them in place in the slots: they may then already be padded
+ * and carry their FCS while their lens are stale.  Zero copy is taken for a
+ * batch only when every frame's room [offset, offset + capacity) lies inside
+ * one slot and no slot holds two of the batch's frames.  lnx_ingress_packets
+ * writes results the same way. */
 #define LNX_TX_CHECKSUM 1u
 #define LNX_TX_FCS 2u
 int lnx_egress_packets(lnx_rx_ring* ring, uint8_t* const* bufs, uint32_t* lens, uint64_t n, uint32_t offset,

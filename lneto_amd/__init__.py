@@ -306,7 +306,6 @@ def _need_len(what, name, t, n):
 
 
 BATCH_SHORT_FRAMES = 1  # LNX_BATCH_SHORT_FRAMES
-SHORT_FRAME_MEAN = 512  # LNX_SHORT_FRAME_MEAN
 
 
 def crc32_batch(d_bytes, d_off, out=None, stream=None, short_frames=False):
@@ -315,8 +314,8 @@ def crc32_batch(d_bytes, d_off, out=None, stream=None, short_frames=False):
     d_bytes: uint8 device tensor; d_off: int64 device tensor of N+1 offsets.
     Returns an int32 device tensor holding the uint32 CRCs bit-for-bit.
     short_frames=True (lnx_crc32_batch_ex with LNX_BATCH_SHORT_FRAMES): the
-    caller knows the mean frame length is under SHORT_FRAME_MEAN bytes; the
-    staged lane-stream kernel reads the batch (same results).
+    staged lane-stream kernel reads every slice that is not giant, where the
+    plain entry picks the kernel per slice on the device (same results).
     """
     import torch
     what = "lnx_crc32_batch_ex" if short_frames else "lnx_crc32_batch"

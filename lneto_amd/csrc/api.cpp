@@ -247,12 +247,18 @@ struct DeviceCtx {
   // Per stream: the staged kernel's giant-slice slots (stage_kernel.hip
   // giant_pieces; zero between launches).  Launches on one stream run in
   // order, so each stream owns one set; streams never share one.
+  // hipStreamPerThread names a different stream in every thread, so it is
+  // keyed by thread too.  At most kGiantStreams sets live per device; the
+  // least recently used one is freed (after a device sync) to make room.
   struct GiantScratch {
     hipStream_t stream;
+    std::thread::id thread;
     uint32_t* p;
+    uint64_t used;  // use counter at the last call
   };
   std::mutex giant_mu;
   std::vector<GiantScratch> giant;
+  uint64_t giant_clock = 0;
 #ifdef LNX_RESEARCH
   // Per-stream scratch of the two-launch TX append (the CRCs between its
   // launches): calls on one stream run in order, so each stream reuses its
@@ -364,22 +370,38 @@ int get_ctx(DeviceCtx** out) {
 // (stage_kernel.hip: at most 2^20 pieces plus one per slice)
 constexpr size_t kGiantSlots = (1u << 20) + 4096u;
 
-// The calling device's giant-slice scratch for `stream`, zeroed once when made.
+// The calling device's giant-slice scratch for `stream`, zeroed on that
+// stream when made (stream order puts the zeroing before the first launch).
+constexpr size_t kGiantStreams = 32;
 int giant_scratch(DeviceCtx* c, hipStream_t stream, uint32_t** out) {
   std::lock_guard<std::mutex> lk(c->giant_mu);
-  for (const auto& g : c->giant)
-    if (g.stream == stream) {
+  const std::thread::id tid = stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
+  ++c->giant_clock;
+  for (auto& g : c->giant)
+    if (g.stream == stream && g.thread == tid) {
+      g.used = c->giant_clock;
       *out = g.p;
       return LNX_OK;
     }
-  uint32_t* p = nullptr;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), 2 * kGiantSlots * sizeof(uint32_t));
-  if (e != hipSuccess) return hip_fail(e, "hipMalloc(giant-slice scratch)");
-  if ((e = hipMemset(p, 0, 2 * kGiantSlots * sizeof(uint32_t))) != hipSuccess) {
-    (void)hipFree(p);
-    return hip_fail(e, "hipMemset(giant-slice scratch)");
+  hipError_t e;
+  if (c->giant.size() >= kGiantStreams) {
+    // its stream may still run a launch on it (or be gone): wait for the device
+    auto lru = std::min_element(c->giant.begin(), c->giant.end(),
+                                [](const DeviceCtx::GiantScratch& a, const DeviceCtx::GiantScratch& b) {
+                                  return a.used < b.used;
+                                });
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize(giant-slice scratch)");
+    (void)hipFree(lru->p);
+    c->giant.erase(lru);
   }
-  c->giant.push_back({stream, p});
+  uint32_t* p = nullptr;
+  e = hipMalloc(reinterpret_cast<void**>(&p), 2 * kGiantSlots * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc(giant-slice scratch)");
+  if ((e = hipMemsetAsync(p, 0, 2 * kGiantSlots * sizeof(uint32_t), stream)) != hipSuccess) {
+    (void)hipFree(p);
+    return hip_fail(e, "hipMemsetAsync(giant-slice scratch)");
+  }
+  c->giant.push_back({stream, tid, p, c->giant_clock});
   *out = p;
   return LNX_OK;
 }

@@ -1540,7 +1540,8 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
   const uint64_t fb1 = fb0 + per_block < nframes ? fb0 + per_block : nframes;
   // the plain entries launch this kernel and the staged one over the same
   // slices (dispatch.hpp): a slice that is not the rows kernel's exits here
-  if (!SEG && policy != kPolicyRows && slice_kind(bytes, off, fb0, fb1, policy) != kSliceRows) return;
+  if (!SEG && policy != kPolicyRows && slice_kind(bytes, off, fb0, fb1, policy, batch_mean(off, nframes)) != kSliceRows)
+    return;
   // byte bounds of frames [f0, f1): offsets mode off[f0], off[f1]; segment
   // mode (frames in address order, not overlapping) start[f0], end of f1 - 1
   auto lo_of = [&](uint64_t f0, uint64_t f1) -> uint64_t { return SEG ? (f1 > f0 ? off[f0] : 0) : off[f0]; };
@@ -1548,6 +1549,22 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
     return SEG ? (f1 > f0 ? off[f1 - 1] + seg_len[f1 - 1] : 0) : off[f1];
   };
   const uint64_t ob0 = lo_of(fb0, fb1), ob1 = hi_of(fb0, fb1);
+  // Segment mode: the pipelined rows address the slice's frames relative to
+  // its first start and store the TX tail through that base, so they need the
+  // slice in address order without overlap, start[i] + len[i] <= start[i + 1].
+  // A slice that is not (any order is legal at the C-ABI) takes the per-frame
+  // path below, which addresses every frame from its own 64-bit start.  The
+  // check's loads overlap the LDS image copy; its verdict is combined through
+  // LDS after the image's barrier.  (A wave-uniform trip count: the audit's
+  // loop rule)
+  bool seg_bad = false;
+  if constexpr (SEG) {
+    for (uint64_t i0 = fb0; i0 < fb1; i0 += kBlockThreads) {  // (clamped indices: no branch, every lane loads)
+      const uint64_t i = i0 + threadIdx.x < fb1 ? i0 + threadIdx.x : fb1 - 1;
+      const uint64_t s = off[i], e = s + seg_len[i], o1 = off[i + 1 < fb1 ? i + 1 : i];
+      seg_bad = seg_bad || (i + 1 < fb1 && e > o1);
+    }
+  }
   int rl = RLF;
   // MIDW (16-lane rows): 1 = one word per lane, 2 = two words, 3 = lean line
   // rows, 4 = lean line rows below kLeanMean, one word per lane above
@@ -1607,6 +1624,14 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
   L.bt = kTBase | (col << 2);
   const uint64_t gwave = (uint64_t)blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __syncthreads();
+  if constexpr (SEG) {
+    // any thread's frame out of order: the whole slice per frame (a spare
+    // dword of the image's zero tail, past the chunk counter)
+    uint32_t* flag = lds_words + kCtrBase / 4 + 16;
+    if (__builtin_amdgcn_ballot_w64(seg_bad) != 0 && (threadIdx.x & 63u) == 0) *flag = 1u;
+    __syncthreads();
+    seg_bad = __builtin_amdgcn_readfirstlane((int)*flag) != 0;  // (uniform: keeps the branch scalar)
+  }
   const char* lds = reinterpret_cast<const char*>(lds_words);
   uint64_t* tl = nullptr;
   if (timeline) {
@@ -1657,8 +1682,9 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
     return cx;
   };
   const Range own = range_of(blockIdx.x, ob0, ob1);
-  if (!own.fits) {
-    // gigabyte frames: static per-wave ranges on the unpipelined path
+  if (!own.fits || seg_bad) {
+    // gigabyte frames, or segments out of address order: static per-wave
+    // ranges on the unpipelined path, each frame from its own start
     const uint64_t fw0 = gwave * frames_per_wave < nframes ? gwave * frames_per_wave : nframes;
     const uint64_t fw1 = fw0 + frames_per_wave < nframes ? fw0 + frames_per_wave : nframes;
     if (narrow && NW4 != 4) {

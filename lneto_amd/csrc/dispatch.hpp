@@ -17,7 +17,8 @@
 //  * kSliceStage: any other mix (every mixed-length distribution measured ran
 //    faster staged, 8-70 %);
 //  * kSliceGiant: the slice's bytes do not fit 31-bit buffer offsets (frames
-//    of gigabytes), or its frames average 1 MiB or more.  All workgroups of
+//    of gigabytes), or its frames average 1 MiB or more, or it spans 16 MiB or
+//    more at 8 times the batch's mean frame length.  All workgroups of
 //    the staged launch fold such slices together in byte pieces
 //    (stage_kernel.hip giant_pieces).
 #pragma once
@@ -42,11 +43,27 @@ constexpr uint64_t kGiantMean = 1ull << 20;
 // many bytes of each other
 constexpr uint32_t kUniformSpread = 8;
 
+// a slice is giant as well when it spans kGiantBig bytes or more and its
+// frames average kGiantSkew times the batch's mean or more: a few large frames
+// among many short ones (a 1.9 GB frame among 65 536 Zipf frames is neither
+// giant by span nor by mean, and one staged block, one wave, would stream it)
+constexpr uint64_t kGiantBig = 16ull << 20;
+constexpr uint64_t kGiantSkew = 8;
+
 // Whether a slice of nf frames spanning `span` bytes from a base `adj` bytes
-// into its 128-byte line is giant (both launches and every workgroup of the
-// staged one evaluate this on the same offsets).
-__host__ __device__ constexpr bool slice_is_giant(uint64_t span, uint64_t adj, uint64_t nf) {
-  return nf > 0 && (span + adj >= kGiantSpan || span >= nf * kGiantMean);
+// into its 128-byte line is giant, in a batch whose frames average `gmean`
+// bytes (both launches and every workgroup of the staged one evaluate this on
+// the same offsets).
+__host__ __device__ constexpr bool slice_is_giant(uint64_t span, uint64_t adj, uint64_t nf, uint64_t gmean) {
+  return nf > 0 &&
+         (span + adj >= kGiantSpan || span >= nf * kGiantMean || (span >= kGiantBig && span >= nf * kGiantSkew * gmean));
+}
+
+// The batch's mean frame length (off[n] - off[0]) / n, 0 when off[n] < off[0]
+// (every workgroup of both launches: the same value).
+__device__ __forceinline__ uint64_t batch_mean(const uint64_t* off, uint64_t n) {
+  const uint64_t o0 = off[0], on = off[n];
+  return on > o0 ? (on - o0) / n : 0;
 }
 
 // The partition both launches use: grid = min(#CU, ceil(n / 64)) workgroups,
@@ -73,12 +90,12 @@ __host__ __device__ constexpr bool rows_length(uint64_t mean) {
 // slice.  A sampled end below its start (offsets out of order) sends the slice
 // to the rows kernel, whose per-frame windows treat such a frame as empty.
 __device__ __forceinline__ uint32_t slice_kind(const uint8_t* bytes, const uint64_t* __restrict__ off, uint64_t fb0,
-                                               uint64_t fb1, uint32_t policy) {
+                                               uint64_t fb1, uint32_t policy, uint64_t gmean) {
   if (fb1 <= fb0) return kSliceNone;
   const uint64_t o0 = off[fb0], o1 = off[fb1];
   const uint64_t span = o1 > o0 ? o1 - o0 : 0;
   const uint64_t adj = (reinterpret_cast<uintptr_t>(bytes) + o0) & 127u;
-  if (slice_is_giant(span, adj, fb1 - fb0)) return kSliceGiant;
+  if (slice_is_giant(span, adj, fb1 - fb0, gmean)) return kSliceGiant;
   if (policy == kPolicyShort) return kSliceStage;
   const uint64_t nf = fb1 - fb0;
   const uint32_t lane = threadIdx.x & 63u;

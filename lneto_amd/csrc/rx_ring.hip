@@ -579,6 +579,7 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
   int rc = LNX_OK;
   std::vector<std::pair<uint64_t, uint32_t>> pending(depth, {0, 0});
   std::vector<bool> in_place(depth, false);  // the stage's batch was patched in the slots (zero copy)
+  std::vector<uint32_t> slot_batch;           // zero copy: the batch (k + 1) that last took each slot
   // A batch's results reach the caller only from a stream that completed: on
   // a failed sync its lens and status stay untouched (and, when it was
   // copied, its frames).
@@ -608,11 +609,19 @@ int lnx_egress_packets(lnx_rx_ring* r, uint8_t* const* bufs, uint32_t* lens, uin
     const uint32_t nb = (uint32_t)std::min<uint64_t>(per, n - i0);
     auto& s = r->st[sk];
     // zero copy when the buffers are the ring's slots (any order): tx_finish
-    // reads each frame in place and patches it there
+    // reads each frame in place and patches it there.  Only when every frame's
+    // room [offset, offset + capacity) lies inside its own slot and no slot
+    // serves two frames of the batch: the kernel's stores into one frame then
+    // cannot race with its loads of another (the copying form gathers every
+    // frame before writing any back, so it stays exact for any buffers).
     bool direct = r->zero_copy;
+    if (direct && slot_batch.size() != r->nslots) slot_batch.assign(r->nslots, 0);
     for (uint32_t j = 0; j < nb && direct; ++j) {
       uint64_t pos = 0;
       direct = in_ring(r, bufs[i0 + j], offset, capacity, &pos);
+      const uint64_t rel = pos - offset, slot = rel / r->cap;
+      direct = direct && rel % r->cap + offset + capacity <= r->cap && slot_batch[slot] != k + 1;
+      if (direct) slot_batch[slot] = k + 1;
       s.h_off[j] = pos;
       s.h_len[j] = lens[i0 + j];
     }

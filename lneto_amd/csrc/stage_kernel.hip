@@ -59,7 +59,9 @@ constexpr uint32_t kSTr = 65536;                        // transposes: 8 KiB per
 constexpr uint32_t kSBnd = kSTr + kStageW * 8192;       // boundary lists
 constexpr uint32_t kSNib = kSBnd + kStageW * kSList;    // Z_{2^m}, m = 0..30: (m, i, v) at 512 m + 64 i + 4 v
 constexpr uint32_t kSCtr = kSNib + 31 * 512;            // the workgroup's block counter
-constexpr uint32_t kSBytes = kSCtr + 16;
+constexpr uint32_t kSGpre = kSCtr + 16;                 // giant slices: frame prefix gpre[0..G] (G <= 256)
+constexpr uint32_t kSBad = kSGpre + 260 * 4;            // giant slices out of order: bit g of 8 dwords
+constexpr uint32_t kSBytes = kSBad + 32;
 static_assert(kSBytes <= 163840, "stage LDS");
 static_assert((kStageBF + 2) % 64 == 0, "whole-wave list loads");
 // compact image in HBM (api.cpp build_stage_image): A[256], B[256], the
@@ -72,8 +74,6 @@ constexpr uint32_t kStageNibHiImg = kStageZ8Img + 2048 + 3072 + 4096;
 // giant slices: pieces of at least this many bytes, at most kGiantPieces of them
 constexpr uint64_t kGiantPieceMin = 16384;
 constexpr uint32_t kGiantPieces = 1u << 20;
-// a frame of an out-of-order block longer than this is not folded (result 0)
-constexpr uint64_t kOooMaxFrame = 1ull << 20;
 
 constexpr uint32_t kSOOB = 0x80000000u;
 constexpr uint32_t kSNone = 0xFFFFFFFFu;
@@ -184,22 +184,80 @@ __device__ __forceinline__ void stage_store(void* out, uint64_t f, uint32_t v) {
     reinterpret_cast<uint8_t*>(out)[f] = (uint8_t)v;
 }
 
+// ---------------------------------------------------------------- one frame, one wave
+// The CRC register (init 0xFFFFFFFF) of bytes [s, e), s < e wave-uniform,
+// folded by the whole wave: [B, e), B = s rounded down to a 16-byte address,
+// is cut into 64 chunks of C bytes (C a multiple of 128); lane k folds the
+// part of chunk k inside [s, e) from 0 (lane 0, whose part starts at s, from
+// the init), 128 bytes a round, and by linearity the frame's register is
+// XOR_k Z_{e - ce_k}(r_k) (ce_k = the end of lane k's part).  Each 16-byte
+// load is aligned and holds a byte of [s, e) (a block past the lane's part
+// re-reads the one at B), so it never leaves the frame's pages.  A round whose
+// 128 bytes some lane does not own whole is folded byte by byte from the
+// wave's staging area `tr` (64 x 128 bytes).  Used for the frames the staged
+// blocks cannot take (out-of-order blocks, giant slices out of order).
+__device__ uint32_t wave_fold(const char* lds, const uint32_t* image, const uint8_t* bytes, uint64_t s, uint64_t e,
+                              char* tr, uint32_t lane, uint32_t b0, const Z8Lane& z8) {
+  const uint64_t B = s - ((reinterpret_cast<uintptr_t>(bytes) + s) & 15u);
+  const uint64_t C = ((e - B + 63u) / 64u + 127u) & ~127ull;
+  const uint64_t c0 = B + (uint64_t)lane * C;
+  const uint64_t cs = c0 > s ? c0 : s, ce = c0 + C < e ? c0 + C : e;
+  const bool has = cs < ce;
+  uint32_t r = lane == 0 ? 0xFFFFFFFFu : 0u;
+  const uint64_t rounds = C / 128u;
+  for (uint64_t t = 0; t < rounds; ++t) {
+    const uint64_t p = c0 + 128u * t;
+    const bool live = has && p < ce;
+    u32x4 w[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      w[m] = *reinterpret_cast<const u32x4*>(bytes + (live && p + 16u * m < ce ? p + 16u * m : B));
+    const bool clean = !live || (p >= cs && p + 128u <= ce);
+    if (__builtin_amdgcn_ballot_w64(!clean) == 0) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const uint32_t nr = s_z8unit(lds, r ^ w[u >> 1][(2 * u) & 3], w[u >> 1][(2 * u + 1) & 3], z8);
+        r = live ? nr : r;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) *reinterpret_cast<u32x4*>(tr + 128u * lane + 16u * m) = w[m];
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = 0; i < 128u; ++i) {
+      const uint64_t pos = p + i;
+      const bool act = live && pos >= cs && pos < ce;
+      const uint32_t byte = (uint32_t)(uint8_t)tr[128u * lane + i];
+      const uint32_t nr = s_z1(lds, r ^ byte, b0);
+      r = act ? nr : r;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  r = s_zd64(lds, image, has ? e - ce : 0u, has ? r : 0u);
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) r ^= (uint32_t)__shfl_xor((int)r, sft);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)r);
+}
+
 // ---------------------------------------------------------------- out of order
 // A block whose offsets are not non-decreasing (outside the entry's contract;
 // a frame whose end is below its start is empty, as in the rows kernel): one
-// lane per frame, byte by byte, the whole wave looping to the longest frame
-// (a lane past its frame re-reads its first byte and keeps its register, so
-// no load issues under narrowed exec — the audit's loop rule).
-// Frames longer than kOooMaxFrame are not folded (result 0 / not ok), which
-// bounds the loop.
+// lane per frame up to kOooLane bytes, byte by byte, the whole wave looping to
+// the longest such frame (a lane past its frame re-reads its first byte and
+// keeps its register, so no load issues under narrowed exec — the audit's
+// loop rule); each longer frame then by the whole wave
+// (wave_fold).  Every frame gets its true CRC.
+constexpr uint64_t kOooLane = 16384;
 template <StageMode MODE>
-__device__ __forceinline__ void ooo_block(const char* lds, const uint8_t* bytes, const uint64_t* off, uint64_t f0, uint32_t bf,
-                          void* out, uint32_t lane, uint32_t b0) {
+__device__ __forceinline__ void ooo_block(const char* lds, const uint32_t* image, const uint8_t* bytes,
+                                          const uint64_t* off, uint64_t f0, uint32_t bf, void* out, char* tr,
+                                          uint32_t lane, uint32_t b0, const Z8Lane& z8) {
   for (uint32_t j0 = 0; j0 < bf; j0 += 64u) {
     const uint32_t j = j0 + lane;
     const uint64_t s = j < bf ? off[f0 + j] : 0, e0 = j < bf ? off[f0 + j + 1] : 0;
     const uint64_t len0 = e0 > s ? e0 - s : 0;
-    const uint64_t len = len0 > kOooMaxFrame ? 0 : len0;
+    const bool by_lane = len0 <= kOooLane;
+    const uint64_t len = by_lane ? len0 : 0;
     uint32_t r = 0xFFFFFFFFu;
     for (uint64_t q = 0;; ++q) {
       const bool act = q < len;
@@ -209,7 +267,13 @@ __device__ __forceinline__ void ooo_block(const char* lds, const uint8_t* bytes,
       const uint32_t nr = s_z1(lds, r ^ b, b0);
       r = act ? nr : r;
     }
-    if (j < bf) stage_store<MODE>(out, f0 + j, len0 > kOooMaxFrame ? 0u : stage_value<MODE>(r, len));
+    if (j < bf && by_lane) stage_store<MODE>(out, f0 + j, stage_value<MODE>(r, len));
+    for (uint64_t big = __builtin_amdgcn_ballot_w64(j < bf && !by_lane); big != 0; big &= big - 1u) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(big);
+      const uint64_t fs = off[f0 + j0 + k], fe = off[f0 + j0 + k + 1];  // (every lane: one address)
+      const uint32_t R = wave_fold(lds, image, bytes, fs, fe, tr, lane, b0, z8);
+      if (lane == 0) stage_store<MODE>(out, f0 + j0 + k, stage_value<MODE>(R, fe - fs));
+    }
   }
 }
 
@@ -228,22 +292,72 @@ __device__ __forceinline__ void ooo_block(const char* lds, const uint8_t* bytes,
 // piece), XORed into the scratch slot of the first piece boundary it crosses
 // (device-scope atomics: the XOR, then a release/acquire count); the lane
 // whose count completes the frame takes the XOR (leaving the slot zero for
-// the next launch) and stores the result.  Offsets must be non-decreasing in
-// giant slices.
+// the next launch) and stores the result.
+//
+// The pieces need a slice's offsets non-decreasing (the entry's contract).
+// So that a batch outside it can neither fault nor leave the scratch dirty for
+// the next launch, the workgroup first checks every giant slice's offsets
+// (frames numbered across the giant slices by the prefix gpre, 512 at a time);
+// a slice with a decreasing pair gets no pieces, and its frames are folded
+// one per wave over the whole grid instead (wave_fold; a frame whose end is
+// below its start is empty, as everywhere).
 template <StageMode MODE>
 __device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* image, const uint8_t* bytes, const uint64_t* off,
-                             uint64_t nframes, uint64_t per, void* out, uint32_t* scratch, char* tr, uint32_t* pre,
-                             uint32_t lane, uint32_t b0, const Z8Lane& z8) {
+                             uint64_t nframes, uint64_t per, uint64_t gmean, void* out, uint32_t* scratch, char* tr,
+                             uint32_t* pre, uint32_t* gpre, uint32_t* badm, uint32_t lane, uint32_t b0,
+                             const Z8Lane& z8) {
   const uint32_t G = gridDim.x;
-  // ---- the giant slices, their total bytes and the piece prefix pre[0..G] (LDS)
+  auto slice = [&](uint32_t w, uint64_t& f0, uint64_t& f1, uint64_t& s, uint64_t& span) -> bool {
+    f0 = (uint64_t)w * per < nframes ? (uint64_t)w * per : nframes;
+    f1 = f0 + per < nframes ? f0 + per : nframes;
+    s = off[f0];
+    const uint64_t e = off[f1];
+    span = e > s ? e - s : 0;
+    const uint64_t adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
+    return w < G && slice_is_giant(span, adj, f1 - f0, gmean);
+  };
+  // ---- the giant slices out of order (bit g of badm)
+  if (threadIdx.x < 64u) {  // wave 0: gpre[w] = frames of the giant slices before w
+    uint32_t carry = 0;
+    for (uint32_t w0 = 0; w0 < G; w0 += 64u) {
+      const uint32_t w = w0 + lane;
+      uint64_t f0, f1, s, span;
+      const bool gi = slice(w, f0, f1, s, span);
+      const uint32_t nf = gi ? (uint32_t)(f1 - f0) : 0u;
+      uint32_t inc = nf;
+#pragma unroll
+      for (int sft = 1; sft < 64; sft <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)inc, sft);
+        inc += lane >= (uint32_t)sft ? o : 0u;
+      }
+      if (w <= G) gpre[w] = carry + inc - nf;
+      carry += (uint32_t)__shfl((int)inc, 63);
+    }
+    if (lane == 0) gpre[G] = carry;
+  }
+  __syncthreads();
+  {
+    const uint32_t TF = gpre[G];
+    for (uint32_t t0 = 0; t0 < TF; t0 += kStageW * 64u) {
+      const uint32_t t = t0 + threadIdx.x;
+      uint32_t g = 0;
+      for (uint32_t step = 256u; step > 0; step >>= 1)
+        if (g + step <= G && gpre[g + step] <= t) g += step;
+      if (t < TF) {
+        const uint64_t i = (uint64_t)g * per + (t - gpre[g]);
+        if (off[i + 1] < off[i]) __hip_atomic_fetch_or(badm + (g >> 5), 1u << (g & 31u), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  __syncthreads();
+  auto bad = [&](uint32_t w) -> bool { return w < G && ((badm[w >> 5] >> (w & 31u)) & 1u) != 0u; };
+  // ---- the in-order giant slices, their total bytes and the piece prefix pre[0..G] (LDS)
   uint64_t tg = 0;
   for (uint32_t w0 = 0; w0 < G; w0 += 64u) {
     const uint32_t w = w0 + lane;
-    const uint64_t f0 = (uint64_t)w * per < nframes ? (uint64_t)w * per : nframes;
-    const uint64_t f1 = f0 + per < nframes ? f0 + per : nframes;
-    const uint64_t s = off[f0], e = off[f1];
-    const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
-    const bool gi = w < G && slice_is_giant(span, adj, f1 - f0);
+    uint64_t f0, f1, s, span;
+    const bool gi = slice(w, f0, f1, s, span) && !bad(w);
     tg += gi ? span : 0;
   }
 #pragma unroll
@@ -256,11 +370,8 @@ __device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* im
   uint32_t carry = 0;
   for (uint32_t w0 = 0; w0 < G; w0 += 64u) {
     const uint32_t w = w0 + lane;
-    const uint64_t f0 = (uint64_t)w * per < nframes ? (uint64_t)w * per : nframes;
-    const uint64_t f1 = f0 + per < nframes ? f0 + per : nframes;
-    const uint64_t s = off[f0], e = off[f1];
-    const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
-    const bool gi = w < G && slice_is_giant(span, adj, f1 - f0);
+    uint64_t f0, f1, s, span;
+    const bool gi = slice(w, f0, f1, s, span) && !bad(w);
     const uint32_t np = gi ? (uint32_t)((span + P - 1) / P) : 0u;
     uint32_t inc = np;  // inclusive scan over the 64 lanes
 #pragma unroll
@@ -395,6 +506,18 @@ __device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* im
     r = runs_on ? z : r;
     frame_end(runs_on, x);
   }
+  // ---- the giant slices out of order: frame i of one to wave i mod NW of the grid
+  const uint32_t W = blockIdx.x * kStageW + (threadIdx.x >> 6), NW = G * kStageW;
+  for (uint32_t g = 0; g < G; ++g) {
+    if (!bad(g)) continue;
+    const uint64_t F0 = (uint64_t)g * per < nframes ? (uint64_t)g * per : nframes;
+    const uint64_t F1 = F0 + per < nframes ? F0 + per : nframes;
+    for (uint64_t i = F0 + W; i < F1; i += NW) {
+      const uint64_t s = off[i], e = off[i + 1];  // (every lane: one address)
+      const uint32_t R = e > s ? wave_fold(lds, image, bytes, s, e, tr, lane, b0, z8) : 0xFFFFFFFFu;
+      if (lane == 0) stage_store<MODE>(out, i, stage_value<MODE>(R, e > s ? e - s : 0u));
+    }
+  }
 }
 
 // ---------------------------------------------------------------- the kernel
@@ -411,7 +534,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   // ---- this workgroup's slice, and whether the launch has giant slices
   // (every workgroup reads the G + 1 slice bounds: L2 hits after the first)
-  const uint32_t own = slice_kind(bytes, off, fb0, fb1, policy);
+  const uint64_t gmean = batch_mean(off, nframes);
+  const uint32_t own = slice_kind(bytes, off, fb0, fb1, policy, gmean);
   bool giant = false;
   for (uint32_t w0 = 0; w0 < gridDim.x; w0 += 64u) {
     const uint32_t w = w0 + lane;
@@ -419,7 +543,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     const uint64_t f1 = f0 + frames_per_wg < nframes ? f0 + frames_per_wg : nframes;
     const uint64_t s = off[f0], e = off[f1];
     const uint64_t span = e > s ? e - s : 0, adj = (reinterpret_cast<uintptr_t>(bytes) + s) & 127u;
-    giant = giant || __builtin_amdgcn_ballot_w64(w < gridDim.x && slice_is_giant(span, adj, f1 - f0)) != 0;
+    giant = giant || __builtin_amdgcn_ballot_w64(w < gridDim.x && slice_is_giant(span, adj, f1 - f0, gmean)) != 0;
   }
   if (own != kSliceStage && !giant) return;
   // ---- image: the T8 values expanded into their 8 bank columns, the nibble tables verbatim
@@ -434,6 +558,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     }
     for (uint32_t i = t; i < 31u * 128u; i += kThreads) reinterpret_cast<uint32_t*>(lds + kSNib)[i] = image[512 + i];
     if (t == 0) *reinterpret_cast<uint32_t*>(lds + kSCtr) = 0;
+    if (t < 8u) reinterpret_cast<uint32_t*>(lds + kSBad)[t] = 0;
   }
   __syncthreads();
   const uint32_t b0 = (lane & 7u) << 2;
@@ -483,7 +608,7 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       ooo = ooo || (j >= 1u && j <= bf && list[j] < list[j - 1u]);
     }
     if (__builtin_amdgcn_ballot_w64(ooo) != 0) {
-      ooo_block<MODE>(lds, bytes, off, f0, bf, out, lane, b0);
+      ooo_block<MODE>(lds, image, bytes, off, f0, bf, out, tr, lane, b0, z8);
       __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next block
       continue;
     }
@@ -748,7 +873,9 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     __builtin_amdgcn_wave_barrier();  // the list is rewritten by the next block
   }
   if (giant)
-    giant_pieces<MODE>(lds, image, bytes, off, nframes, frames_per_wg, out, scratch, tr, list, lane, b0, z8);
+    giant_pieces<MODE>(lds, image, bytes, off, nframes, frames_per_wg, gmean, out, scratch, tr, list,
+                       reinterpret_cast<uint32_t*>(lds + kSGpre), reinterpret_cast<uint32_t*>(lds + kSBad), lane, b0,
+                       z8);
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,

@@ -117,7 +117,7 @@ def test_tx_finish_mtu_round_trip(cuda):
 
 def test_tx_finish_equals_the_two_calls_at_scale(cuda):
     """256 Ki frames (the generated ones of every kind, tiled in random order,
-    at random leads in 2048-B slots): the same bytes, lengths and statuses as
+    at random leads in 2048-B slots taken in shuffled order): the same bytes, lengths and statuses as
     lnx_tx_checksum_batch then lnx_fcs_append_batch, over 5462 groups."""
     import torch
     import lneto_amd as L
@@ -127,10 +127,11 @@ def test_tx_finish_equals_the_two_calls_at_scale(cuda):
     n = 1 << 18
     pick = rng.integers(0, len(base), n)
     lead = rng.integers(0, 16, n)
-    # slots in increasing address order: lnx_fcs_append_batch's precondition
-    # (lneto_amd.h; tx_finish itself takes any order, test_tx_finish_matches_oracle)
+    # slots in shuffled order (round 5 had to keep them sorted: out-of-order
+    # starts faulted the append entry, r6p; its workgroups now fold such a
+    # slice frame by frame)
     buf = rng.integers(0, 256, SLOT * n + 64, dtype=np.uint8)
-    starts = (np.arange(n, dtype=np.int64) * SLOT + lead).astype(np.int64)
+    starts = (rng.permutation(n).astype(np.int64) * SLOT + lead).astype(np.int64)
     lens = np.array([len(base[i]) for i in pick], dtype=np.int32)
     arrs = [np.frombuffer(f, np.uint8) for f in base]
     for k in range(n):
