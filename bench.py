@@ -260,6 +260,36 @@ def _udp4_frames(synth, n, cap, lens):
     return rows
 
 
+def _udp4_device(L, torch, d_bytes, starts, lens, fcs: bool, chunk: int = 1 << 20):
+    """Valid UDP/IPv4 frames in place on the device: frame i = d_bytes[starts[i] :
+    starts[i] + lens[i]] (int64 / int64 device tensors) gets an Ethernet + IPv4 +
+    UDP header whose length fields cover the frame (without its last 4 bytes
+    when `fcs`), its IPv4 header and UDP checksums (lnx_tx_checksum_batch) and,
+    when `fcs`, its LE FCS in the last 4 bytes (lnx_crc32_segments), so the
+    receive check accepts every frame.  Headers in chunks of `chunk` frames
+    (an index tensor of 42 entries per frame)."""
+    dev = d_bytes.device
+    body = lens - 4 if fcs else lens
+    hdr = torch.tensor(list(bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0, 0, 0])
+                            + bytes.fromhex("123440004011000" + "0c0a80a01c0a80a02")
+                            + bytes.fromhex("14e9003500000000")), dtype=torch.uint8, device=dev)
+    col = torch.arange(42, device=dev)
+    for a in range(0, starts.numel(), chunk):
+        st, bl = starts[a:a + chunk], body[a:a + chunk]
+        h = hdr.repeat(st.numel(), 1)
+        ip, udp = bl - 14, bl - 34
+        h[:, 16], h[:, 17] = (ip >> 8).to(torch.uint8), (ip & 255).to(torch.uint8)
+        h[:, 38], h[:, 39] = (udp >> 8).to(torch.uint8), (udp & 255).to(torch.uint8)
+        d_bytes[(st[:, None] + col).reshape(-1)] = h.reshape(-1)
+    st = L.tx_checksum_batch(d_bytes, starts, body.to(torch.int32))
+    assert int(st.max()) == 0, "UDP/IPv4 frame construction"
+    if fcs:
+        c = L.crc32_segments(d_bytes, starts, body.to(torch.int32))
+        for a in range(0, starts.numel(), chunk):
+            pos = (starts[a:a + chunk] + body[a:a + chunk])[:, None] + torch.arange(4, device=dev)
+            d_bytes[pos.reshape(-1)] = c[a:a + chunk].view(torch.uint8).view(-1)
+
+
 def packets_bench(args, L, synth, torch, dev, world):
     """The netdev batch boundary end to end (x/netdev/interface.go:85-89,
     DESIGN.md §4): per-frame pageable host buffers, as a Go stack hands them
@@ -469,6 +499,7 @@ def main():
     else:
         off_np = synth.fixed_offsets(n_local, flen)
     nbytes = int(off_np[-1])
+    zipf_slots = False  # --op tx_finish on the Zipf mix: frames in slots, off_np the slot grid
     d_bytes = synth.bytes_torch(nbytes, dev, seed=synth.SEED + lo * 0x10001)
     d_off = torch.from_numpy(off_np.astype(np.int64)).to(dev)
     d_crc = torch.empty(n_local, dtype=torch.int32, device=dev)
@@ -484,13 +515,25 @@ def main():
         d_sum = torch.empty(n_local, dtype=torch.int16, device=dev)
     elif args.op == "fcs_verify":
         d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+    elif args.op == "tx_finish" and flen is None:
+        # the transmit tail on the Zipf mix: frame i (its wire length less the
+        # FCS, >= 60 B: no padding) in a 1536-byte slot, valid UDP/IPv4 headers
+        cap = 1536
+        n_slots = n_local
+        wire = torch.from_numpy(lens.astype(np.int64)).to(dev)
+        d_bytes = synth.bytes_torch(n_slots * cap, dev, seed=synth.SEED + lo * 0x10001)
+        d_start = torch.arange(n_slots, dtype=torch.int64, device=dev) * cap
+        _udp4_device(L, torch, d_bytes, d_start, wire - 4, fcs=False)
+        d_len0 = (wire - 4).to(torch.int32)
+        d_len = d_len0.clone()
+        d_status = torch.empty(n_slots, dtype=torch.uint8, device=dev)
+        nbytes = int((wire - 4).sum())
+        zipf_slots = True
     elif args.op == "tx_finish":
         # the transmit tail in one read (lnx_tx_finish_batch): UDP/IPv4 frames of
         # flen - 4 bytes in CAP-byte slots get their length fields and checksums
         # (idempotent) and their LE FCS in place; the lengths are restored first
         # every step (a 4-byte-per-frame device copy, timed)
-        if flen is None:
-            raise SystemExit("--op tx_finish needs fixed-size frames")
         cap = 1536
         n_slots = n_local
         d_bytes = synth.bytes_torch(n_slots * cap, dev, seed=synth.SEED + lo * 0x10001)
@@ -532,9 +575,20 @@ def main():
         fcs = L.crc32_segments(d_bytes, starts, lens)
         fr[:, flen - 4:] = fcs.view(torch.uint8).view(n_local, 4)
         d_hit = torch.empty(n_local, dtype=torch.int64, device=dev)
+    elif args.op in ("ingress", "tx_checksum", "rx_verify") and flen is None:
+        # the Zipf mix (64-1500 B on the wire) packed back to back: every frame a
+        # valid UDP/IPv4 packet (rx_verify: with its LE FCS), so each takes the
+        # full header-sum + UDP-sum path and is accepted
+        d_lens = d_off[1:] - d_off[:-1]
+        _udp4_device(L, torch, d_bytes, d_off[:-1].contiguous(), d_lens, fcs=args.op == "rx_verify")
+        d_ok = torch.empty(n_local, dtype=torch.uint8, device=dev)
+        d_verdict = torch.empty(n_local, dtype=torch.uint8, device=dev)
+        if args.op == "tx_checksum":
+            d_seg = d_off[:-1].contiguous()
+            d_len = d_lens.to(torch.int32)
     elif args.op in ("ingress", "tx_checksum", "rx_verify"):
-        if flen is None or flen < 42:
-            raise SystemExit(f"--op {args.op} needs fixed-size frames of at least 42 bytes")
+        if flen < 42:
+            raise SystemExit(f"--op {args.op} needs frames of at least 42 bytes")
         fr = d_bytes[: n_local * flen].view(n_local, flen)
         hdr = bytes.fromhex("c0ffee00dead4e8b3af9fb6b0800") + bytes([0x45, 0]) + (flen - 14).to_bytes(2, "big") \
             + bytes.fromhex("12344000401100 00c0a80a01c0a80a02".replace(" ", "")) \
@@ -763,8 +817,10 @@ def main():
         for i in idx:
             s, e = int(off_np[i]), int(off_np[i + 1])
             if args.op in ("fcs_append", "tx_finish"):
-                fr = d_bytes[s:s + flen].cpu().numpy().tobytes()
-                assert int(got[i]) == 0 and int(lens_after[i]) == flen, f"frame {i}: status / length"
+                fl = int(lens[i]) if zipf_slots else flen
+                s = i * 1536 if zipf_slots else s
+                fr = d_bytes[s:s + fl].cpu().numpy().tobytes()
+                assert int(got[i]) == 0 and int(lens_after[i]) == fl, f"frame {i}: status / length"
                 assert O.crc32(fr[:-4]) == int.from_bytes(fr[-4:], "little"), f"mismatch frame {i}"
                 if args.op == "tx_finish":  # the finished frame is a fixed point of both steps and is accepted
                     regen, st = O.tx_checksum(fr[:-4])

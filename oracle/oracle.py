@@ -428,6 +428,39 @@ def tx_checksum(frame: bytes) -> tuple[bytes, int]:
     return bytes(frame), 0
 
 
+def fix_ip_tcp_crcs(frame: bytes) -> tuple[bytes, bool]:
+    """fixIPTCPCRCs of lneto's stack fuzz test (x/xnet/xnet_fuzz_test.go:150-185),
+    which regenerates the checksums of a fuzzed frame before the stack sees it:
+    for an IPv4 EtherType with version 4, IHL >= 5, IHL*4 <= total length <=
+    len(frame), the header CRC over the first 20 bytes (ipv4/frame.go:144-146);
+    then, for TCP with a >= 20-byte IP payload (ipv4 Frame.Payload, frame.go:188-192:
+    bytes [IHL*4, total length) of the Ethernet payload; tcp.NewFrame), the TCP
+    CRC = CRCWriteTCPPseudo + PayloadSum16 of that payload with its CRC field
+    zeroed.  Returns (the frame as the harness leaves it, fixable).  A total
+    length past len(frame) - 14 makes the Go slice run past the frame into the
+    harness's buffer: such a frame is returned unchanged with None (its result
+    depends on bytes outside it)."""
+    f = bytearray(frame)
+    if len(f) < 14 or _be16(f, 12) != ETHERTYPE_IPV4 or len(f) - 14 < 20:  # ethernet / ipv4 NewFrame
+        return bytes(frame), False
+    v, ihl, tl = f[14] >> 4, f[14] & 0xF, _be16(f, 16)
+    if v != 4 or ihl < 5 or tl < ihl * 4 or tl > len(f):
+        return bytes(frame), False
+    if 14 + tl > len(f):
+        return bytes(frame), None
+    _put16(f, 24, 0)
+    _put16(f, 24, ipv4_header_sum16(bytes(f[14:34])))
+    if f[23] != IPPROTO_TCP:
+        return bytes(f), False
+    la = 14 + ihl * 4
+    payload = f[la:14 + tl]
+    if len(payload) < 20:                              # tcp.NewFrame (tcp/frame.go:19-24)
+        return bytes(f), False
+    _put16(f, la + 16, 0)
+    _put16(f, la + 16, ipv4_tcp_pseudo(bytes(f[14:])).payload_sum16(bytes(f[la:14 + tl])))
+    return bytes(f), True
+
+
 # ------------------------------------------------------------ TX FCS append
 ERR_SHORT_BUFFER = 6
 
