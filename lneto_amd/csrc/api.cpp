@@ -17,9 +17,11 @@
 
 namespace lnx {
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
-                               bool verify, const void* image, int num_cus, hipStream_t stream, uint32_t policy);
+                               bool verify, const void* image, int num_cus, hipStream_t stream, uint32_t policy,
+                               uint32_t* stage_flag, uint32_t epoch);
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream);
+                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream,
+                              const uint32_t* stage_flag, uint32_t epoch);
 #ifdef LNX_RESEARCH
 namespace rs {
 hipError_t launch_crc32_stage_research(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
@@ -254,7 +256,8 @@ struct DeviceCtx {
     hipStream_t stream;
     std::thread::id thread;
     uint32_t* p;
-    uint64_t used;  // use counter at the last call
+    uint64_t used;   // use counter at the last call
+    uint32_t epoch;  // the last call's epoch (the staged launch's flag word, kStageFlag)
   };
   std::mutex giant_mu;
   std::vector<GiantScratch> giant;
@@ -367,20 +370,27 @@ int get_ctx(DeviceCtx** out) {
 }
 
 // Slots of the giant slices: acc[kGiantSlots] then cnt[kGiantSlots]
-// (stage_kernel.hip: at most 2^20 pieces plus one per slice)
+// (stage_kernel.hip: at most 2^20 pieces plus one per slice), then the flag
+// word through which the rows launch tells the staged launch it has work
+// (the call's epoch: nonzero, new every call on the stream, so the word needs
+// no reset)
 constexpr size_t kGiantSlots = (1u << 20) + 4096u;
+constexpr size_t kStageFlag = 2 * kGiantSlots;
+constexpr size_t kScratchWords = kStageFlag + 16;
 
 // The calling device's giant-slice scratch for `stream`, zeroed on that
 // stream when made (stream order puts the zeroing before the first launch).
 constexpr size_t kGiantStreams = 32;
-int giant_scratch(DeviceCtx* c, hipStream_t stream, uint32_t** out) {
+int giant_scratch(DeviceCtx* c, hipStream_t stream, uint32_t** out, uint32_t* epoch) {
   std::lock_guard<std::mutex> lk(c->giant_mu);
   const std::thread::id tid = stream == hipStreamPerThread ? std::this_thread::get_id() : std::thread::id();
   ++c->giant_clock;
   for (auto& g : c->giant)
     if (g.stream == stream && g.thread == tid) {
       g.used = c->giant_clock;
+      g.epoch = g.epoch + 1u == 0u ? 1u : g.epoch + 1u;
       *out = g.p;
+      *epoch = g.epoch;
       return LNX_OK;
     }
   hipError_t e;
@@ -395,14 +405,15 @@ int giant_scratch(DeviceCtx* c, hipStream_t stream, uint32_t** out) {
     c->giant.erase(lru);
   }
   uint32_t* p = nullptr;
-  e = hipMalloc(reinterpret_cast<void**>(&p), 2 * kGiantSlots * sizeof(uint32_t));
+  e = hipMalloc(reinterpret_cast<void**>(&p), kScratchWords * sizeof(uint32_t));
   if (e != hipSuccess) return hip_fail(e, "hipMalloc(giant-slice scratch)");
-  if ((e = hipMemsetAsync(p, 0, 2 * kGiantSlots * sizeof(uint32_t), stream)) != hipSuccess) {
+  if ((e = hipMemsetAsync(p, 0, kScratchWords * sizeof(uint32_t), stream)) != hipSuccess) {
     (void)hipFree(p);
     return hip_fail(e, "hipMemsetAsync(giant-slice scratch)");
   }
-  c->giant.push_back({stream, tid, p, c->giant_clock});
+  c->giant.push_back({stream, tid, p, c->giant_clock, 1u});
   *out = p;
+  *epoch = 1u;
   return LNX_OK;
 }
 
@@ -420,11 +431,17 @@ int crc_offsets(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, void*
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
   uint32_t* scratch = nullptr;
-  if ((st = giant_scratch(c, stream, &scratch)) != LNX_OK) return st;
+  uint32_t epoch = 0;
+  if ((st = giant_scratch(c, stream, &scratch, &epoch)) != LNX_OK) return st;
   hipError_t e = hipSuccess;
-  if (policy == kPolicyAuto) e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus, stream, policy);
+  // auto: the rows launch stores the epoch in the flag word when a slice is
+  // not its own, and the staged launch behind it exits at once otherwise
+  uint32_t* flag = policy == kPolicyAuto ? scratch + kStageFlag : nullptr;
+  if (policy == kPolicyAuto)
+    e = launch_crc32_frames(d_bytes, d_off, n, d_out, verify, c->d_image, c->num_cus, stream, policy, flag, epoch);
   if (e != hipSuccess) return hip_fail(e, "crc32_rows_kernel launch");
-  e = launch_crc32_stage(d_bytes, d_off, n, d_out, verify, policy, c->d_stage, scratch, c->num_cus, stream);
+  e = launch_crc32_stage(d_bytes, d_off, n, d_out, verify, policy, c->d_stage, scratch, c->num_cus, stream, flag,
+                         epoch);
   if (e != hipSuccess) return hip_fail(e, "crc32_stage_kernel launch");
   return LNX_OK;
 }

@@ -1518,8 +1518,8 @@ constexpr uint64_t kLineMean = 4096;
 // (MIDW = 4): one frame per row per slot needs frames of at most KSL lines.
 constexpr uint64_t kLeanMean = 1600;
 #ifdef LNX_RESEARCH  // the losing short-frame designs: research library only
-#include "stream_rows.hpp"
-#include "stream_lanes.hpp"
+#include "research/stream_rows.hpp"
+#include "research/stream_lanes.hpp"
 #endif
 
 template <CrcMode MODE, int VAR = 0, int RLF = 0, int KSW = 24, int SW = 1, int KS4 = 16, int S4 = 2,
@@ -1530,7 +1530,8 @@ __global__ void __launch_bounds__(kBlockThreads, 1)
 crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the FCS through it */ const uint64_t* __restrict__ off, uint64_t nframes,
                   uint64_t frames_per_wave, const uint4* __restrict__ images, void* __restrict__ out,
                   uint64_t* __restrict__ timeline,
-                  const uint32_t* seg_len, uint32_t cap, uint32_t policy) {
+                  const uint32_t* seg_len, uint32_t cap, uint32_t policy, uint32_t* __restrict__ stage_flag,
+                  uint32_t epoch) {
   __shared__ __attribute__((aligned(16))) uint32_t lds_words[kLdsDwords];
   // profiling (tools/prof/timeline.py): per wave, 100 MHz clock at entry,
   // after the LDS image copy and at exit; null in the product path
@@ -1540,8 +1541,16 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
   const uint64_t fb1 = fb0 + per_block < nframes ? fb0 + per_block : nframes;
   // the plain entries launch this kernel and the staged one over the same
   // slices (dispatch.hpp): a slice that is not the rows kernel's exits here
-  if (!SEG && policy != kPolicyRows && slice_kind(bytes, off, fb0, fb1, policy, batch_mean(off, nframes)) != kSliceRows)
-    return;
+  // slices: the staged launch behind this one reads one word before anything
+  // else and exits at once unless some workgroup here stored this call's
+  // epoch there (its slice is the staged kernel's, or giant)
+  if (!SEG && policy != kPolicyRows) {
+    const uint32_t kind = slice_kind(bytes, off, fb0, fb1, policy, batch_mean(off, nframes));
+    if (kind != kSliceRows) {
+      if (kind != kSliceNone && stage_flag && threadIdx.x == 0) *stage_flag = epoch;
+      return;
+    }
+  }
   // byte bounds of frames [f0, f1): offsets mode off[f0], off[f1]; segment
   // mode (frames in address order, not overlapping) start[f0], end of f1 - 1
   auto lo_of = [&](uint64_t f0, uint64_t f1) -> uint64_t { return SEG ? (f1 > f0 ? off[f0] : 0) : off[f0]; };
@@ -1579,7 +1588,7 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
   const bool narrow = rl == 4;
   // whole-line windows: the RL = 32 image
   const bool line = rl == 32 || (rl == 16 && (MIDW == 2 || lean));
-  // streaming rows (stream_rows.hpp) for the narrow rows' frames in offsets
+  // streaming rows (research/stream_rows.hpp) for the narrow rows' frames in offsets
   // mode, when the slice's bytes fit 31-bit buffer offsets from a line-aligned base
   bool strm = STR != 0 && narrow && !SEG && MODE != CrcMode::kAppend;
   if (strm) {
@@ -1738,7 +1747,8 @@ crc32_rows_kernel(const uint8_t* bytes,  /* not __restrict__: kAppend writes the
 
 hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,
                        const void* images, int num_cus, hipStream_t stream, uint64_t* timeline = nullptr,
-                       const uint32_t* seg_len = nullptr, uint32_t cap = 0, uint32_t policy = kPolicyRows) {
+                       const uint32_t* seg_len = nullptr, uint32_t cap = 0, uint32_t policy = kPolicyRows,
+                       uint32_t* stage_flag = nullptr, uint32_t epoch = 0) {
   const bool verify = mode == CrcMode::kVerify;
   if (n == 0) return hipSuccess;
   // the slices of dispatch.hpp (the staged launch uses the same): at least
@@ -1751,7 +1761,7 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
   const dim3 g((unsigned)grid), b(kBlockThreads);
 #define LNX_LAUNCH(M, ...) \
   hipLaunchKernelGGL((crc32_rows_kernel<M, __VA_ARGS__>), g, b, 0, stream, bytes, off, n, fpw, img, out, \
-                     timeline, seg_len, cap, policy)
+                     timeline, seg_len, cap, policy, stage_flag, epoch)
   if (seg_len) {  // segment mode (lnx_crc32_segments, the TX FCS append, the receive ring)
     // (every lean-row step non-temporal, EP = 0, was measured no faster for
     // ring slots and is not built: profiles/r2s2r_segment_ep_rejected.txt)
@@ -1858,7 +1868,7 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 139: LNX_W4(0, 3, 2, 32, 1); break;
       case 140: LNX_W4(0, 5, 2, 32, 1); break;
 #undef LNX_W4
-      // streaming rows (stream_rows.hpp) for the narrow rows' frames, under the product dispatch
+      // streaming rows (research/stream_rows.hpp) for the narrow rows' frames, under the product dispatch
       case 150: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
       // its loads + chain only (no frame boundaries), loads only
       case 151: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 1); break;
@@ -1867,7 +1877,7 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
       case 153: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
       case 154: LNX_LAUNCH(CrcMode::kCrc, 151, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
       case 155: LNX_LAUNCH(CrcMode::kCrc, 152, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 2); break;
-      // lane streams (stream_lanes.hpp): full, loads only, loads + chain only
+      // lane streams (research/stream_lanes.hpp): full, loads only, loads + chain only
       case 160: LNX_LAUNCH(CrcMode::kCrc, 0, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
       case 161: LNX_LAUNCH(CrcMode::kCrc, 161, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
       case 162: LNX_LAUNCH(CrcMode::kCrc, 162, 0, 24, 1, 16, 2, 4, 32, false, 4, 24, 1, 4, 13, 2, true, 1, true, 4, 1, 3); break;
@@ -1886,9 +1896,10 @@ hipError_t launch_rows(int var, CrcMode mode, const uint8_t* bytes, const uint64
 
 // Host-side launch helpers (called from api.cpp).
 hipError_t launch_crc32_frames(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                               const void* images, int num_cus, hipStream_t stream, uint32_t policy) {
+                               const void* images, int num_cus, hipStream_t stream, uint32_t policy,
+                               uint32_t* stage_flag, uint32_t epoch) {
   return launch_rows(0, verify ? CrcMode::kVerify : CrcMode::kCrc, bytes, off, n, out, images, num_cus, stream,
-                     nullptr, nullptr, 0, policy);
+                     nullptr, nullptr, 0, policy, stage_flag, epoch);
 }
 #ifdef LNX_RESEARCH
 hipError_t launch_crc32_variant(int var, const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out,

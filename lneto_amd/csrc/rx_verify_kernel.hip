@@ -30,16 +30,19 @@ namespace lnx {
 namespace {
 
 #ifndef LNX_TX_BLOCK
-#define LNX_TX_BLOCK 768
+#define LNX_TX_BLOCK 1024
 #endif
 constexpr int kRvBlock = 1024;
-// the transmit kernel wants more registers than 16 waves of 128 VGPRs give it:
-// there hipcc spills 120-130 bytes per lane to scratch, inside the row passes
-// (memory traffic 1.57 x the frame bytes, 0.71 ms on 1 M x 1500 B); 12 waves of
-// 168 VGPRs spill nothing (1.035 x, 0.48 ms; profiles/r5v_*).  Over host memory
-// (the ring's zero-copy egress, PCIe-bound) 12 and 16 waves measured alike:
-// 17.4-24.5 GiB/s on the Zipf mix, the second process of a pair faster
-// whichever it ran (tools/prof/r5w.sh, r5y.sh)
+// Round 5: the transmit kernel wanted more registers than 16 waves of 128
+// VGPRs give it (hipcc spilled 120-130 bytes per lane inside the row passes:
+// traffic 1.57 x, 0.71 ms on 1 M x 1500 B), so it ran 12 waves of 168 VGPRs
+// (1.035 x, 0.48 -> 0.434 ms; profiles/r5v_*).  Round 6: with 4 qwords of the
+// next pass loaded ahead (kTxPf, was 8) and 48-frame groups (kTxGroup, was
+// 64: the 16 waves' staging fits LDS beside the tables) it takes 126 VGPRs
+// with no scratch, 16 waves: 0.436 -> 0.416 ms on 1 M x 1500 B, 4.50 -> 4.14
+// ms on the 16 M Zipf mix (tools/prof/lib_ab.py).  Over host
+// memory (the ring's zero-copy egress, PCIe-bound) 12 and 16 waves measured
+// alike: 17.4-24.5 GiB/s on the Zipf mix (tools/prof/SESSIONS.md r5w, r5y).
 constexpr int kTxBlock = LNX_TX_BLOCK;
 #ifndef LNX_TX_BLOCK_HOST
 #define LNX_TX_BLOCK_HOST 768
@@ -184,16 +187,24 @@ __device__ __forceinline__ uint32_t rv_dot2(uint32_t w, uint32_t acc) {
 // load crosses the frame's qwords and none is under a branch; the offsets of
 // a group are loaded once, by the lane of each frame.
 // the most frames per wave and group (LDS: tables + the waves' group staging
-// <= 160 KiB): 56 for the receive kernel (16 waves: 154 KiB), 64 for the
-// transmit kernel (12 waves: 155 KiB); the launchers pick the size per batch
-// (balanced_group): on 1 M frames fixed sizes measured 0.331 / 0.310 / 0.322 /
-// 0.340 ms (48 / 52 / 56 / 60, receive) and 0.462 / 0.467 / 0.435 / 0.454 ms
-// (48 / 56 / 60 / 64, transmit) -- the rounds of groups times the group size
-// (tools/prof/r6r.sh, r6u.sh)
+// <= 160 KiB): 56 for the receive kernel (16 waves: 154 KiB), 48 for the
+// transmit kernel (16 waves: 152 KiB; 64 at its round-5 12 waves); the
+// launchers pick the size per batch (balanced_group): on 1 M frames fixed
+// sizes measured 0.331 / 0.310 / 0.322 / 0.340 ms (48 / 52 / 56 / 60,
+// receive) and 0.462 / 0.467 / 0.435 / 0.454 ms (48 / 56 / 60 / 64, transmit
+// at 12 waves) -- the rounds of groups times the group size
+// (tools/prof/SESSIONS.md r6r, r6u)
 constexpr uint32_t kRvGroup = 56;
-constexpr uint32_t kTxGroup = 64;
+#ifndef LNX_TX_GROUP
+#define LNX_TX_GROUP 48
+#endif
+constexpr uint32_t kTxGroup = LNX_TX_GROUP;
 constexpr uint32_t kRvHead = 9;    // staged qwords per frame: frame bytes [0, 72 - mis) >= [0, 65)
-constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead (transmit)
+constexpr int kRvPf = 8;           // qwords per lane of the next pass loaded ahead (host memory)
+#ifndef LNX_TX_PF
+#define LNX_TX_PF 4
+#endif
+constexpr int kTxPf = LNX_TX_PF;   // ... (the transmit kernel over device memory)
 #ifndef LNX_RV_PF_RX
 #define LNX_RV_PF_RX 12
 #endif
@@ -239,6 +250,11 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       x = min(x, __shfl_xor(x, 32));
       return __builtin_amdgcn_readfirstlane(x);
     };
+    auto wave_max = [&](int32_t x) -> int32_t {
+      x = max(x, __shfl_xor(x, 16));
+      x = max(x, __shfl_xor(x, 32));
+      return __builtin_amdgcn_readfirstlane(x);
+    };
     auto prefetch = [&](int slot, uint32_t jn) {
       if (4u * jn >= nrow) return;  // (wave-uniform)
       row_frame(jn, frn[slot], Ltn[slot]);
@@ -257,10 +273,13 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
         pf[slot][PQ - 1] = rv_ld(q < Q2 ? b2 + q : zero);
         asm volatile("");
       } else {
+        // short frames (the Zipf mix): only the units some row's frame reaches
+        // are loaded (a wave-uniform count), the rest are zero without a load
+        const int32_t um = (wave_max(Q2) + 15) >> 4;
 #pragma unroll
         for (int u = 0; u < PQ; ++u) {
           const int32_t q = (int32_t)p + 16 * u;
-          pf[slot][u] = rv_ld(q < Q2 ? b2 + q : zero);
+          pf[slot][u] = u < um ? rv_ld(q < Q2 ? b2 + q : zero) : make_uint2(0u, 0u);
         }
       }
     };
@@ -282,6 +301,9 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       nit = max(nit, __shfl_xor(nit, 32));
       nit = __builtin_amdgcn_readfirstlane(nit);
       qmin = wave_min(qmin);
+      // the units (qwords per lane) any row's CRC window reaches: the later ones
+      // fold nothing and are skipped (wave-uniform)
+      const int32_t nlw = wave_max(NL), qmw = (wave_max(QE) + 15) >> 4;
       uint32_t r = 0, S = 0;
       // the qwords holding the bytes at or past L (the FCS, the last qword's
       // bytes past the frame) went into S, those past Lt into the CRC of lines
@@ -336,7 +358,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
 #pragma unroll
             for (int u = PQ; u < kRvUnroll; ++u) {
               const int32_t q = (int32_t)p + 16 * u;
-              y[u] = rv_ld(q < QE ? base2 + q : zero);
+              y[u] = u < qmw ? rv_ld(q < QE ? base2 + q : zero) : make_uint2(0u, 0u);
             }
           }
         }
@@ -357,7 +379,8 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
           for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, 0, true);
         } else {
 #pragma unroll
-          for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, 0, u < NL);
+          for (int u = 0; u < kRvUnroll; ++u)
+            if (u == 0 || u < nlw) fold(y[u], u, 0, u < NL);
         }
       }
       for (int32_t it = 1; it < nit; ++it) {
@@ -807,7 +830,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
     const uint32_t nrow = (uint32_t)(n - g * gsz < gsz ? n - g * gsz : gsz);
-    rv_rows<FCS, true, HOST>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
+    rv_rows<FCS, true, HOST, HOST ? kRvPf : kTxPf>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
     __builtin_amdgcn_wave_barrier();
 
     // ---------------------------------------------------------------- B: one lane per frame

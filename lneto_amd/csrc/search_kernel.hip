@@ -36,68 +36,6 @@ __device__ __forceinline__ uint32_t zlevel(const uint32_t* lds, int k, uint32_t 
   return z[x & 0xFFu] ^ z[256 + ((x >> 8) & 0xFFu)] ^ z[512 + ((x >> 16) & 0xFFu)] ^ z[768 + (x >> 24)];
 }
 
-#ifdef LNX_RESEARCH  // the r1 word-lane kernel (LNX_PROF_SEARCH=w)
-__global__ void __launch_bounds__(kSearchBlock)
-crc32_search_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                    const int64_t* __restrict__ min_off, uint64_t n, const uint32_t* __restrict__ tables,
-                    int64_t* __restrict__ result) {
-  __shared__ uint32_t lds[kSearchTabBytes / 4];
-  for (uint32_t i = threadIdx.x; i < kSearchTabBytes / 4; i += kSearchBlock) lds[i] = tables[i];
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t nwaves = (uint64_t)gridDim.x * (kSearchBlock / 64);
-  for (uint64_t c = (uint64_t)blockIdx.x * (kSearchBlock / 64) + (threadIdx.x >> 6); c < n; c += nwaves) {
-    const uint64_t s = off[c], e = off[c + 1];
-    const int64_t L = e > s ? (int64_t)(e - s) : 0;
-    int64_t m = min_off ? min_off[c] : 0;
-    if (m < 0) m = 0;
-    int64_t found = -1;
-    if (L >= m + 4) {
-      const uint8_t* d = bytes + s;
-      uint32_t carry = 0xFFFFFFFFu;  // register entering the block (CRC init)
-      // only blocks that can hold a state index k in [m + 4, L] matter, but the
-      // register has to be carried from the start
-      for (int64_t B = 0; B < L && found < 0; B += 256) {
-        const int64_t base = B + 4 * (int64_t)lane;
-        uint32_t w = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w |= (base + q < L ? (uint32_t)d[base + q] : 0u) << (8 * q);
-        // inclusive scan of the word registers (carry folded into word 0: exact
-        // after whole words only)
-        uint32_t a = zlevel(lds, 0, lane == 0 ? w ^ carry : w);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const uint32_t dd = 1u << k;
-          // a holds the words (lane - 2^k, lane]; the partial ending at lane - 2^k
-          // is advanced over those 4*2^k bytes and folded in
-          const uint32_t prev = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - dd) * 4u), (int)a);
-          a ^= lane >= dd ? zlevel(lds, k, prev) : 0u;
-        }
-        // register before this lane's word (the carry itself for word 0), then
-        // per-byte states over the unmodified bytes
-        uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 1u) * 4u), (int)a);
-        r = lane == 0 ? carry : r;
-        int64_t best = -1;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          r = lds[(r ^ (w >> (8 * q))) & 0xFFu] ^ (r >> 8);
-          const int64_t k = base + q + 1;  // bytes consumed
-          if (best < 0 && r == kResidueRegister && k >= m + 4 && k <= L) best = k - 4;
-        }
-        // first hit of the wave: lanes are in byte order, and within a lane q is
-        const uint64_t hits = __builtin_amdgcn_ballot_w64(best >= 0);
-        if (hits) {
-          const uint32_t first = (uint32_t)__builtin_ctzll(hits);
-          found = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)best, first)) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)best >> 32), first) << 32));
-        }
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)a, 63);
-      }
-    }
-    if (lane == 0) result[c] = found;
-  }
-}
-#endif  // LNX_RESEARCH
 
 // ------------------------------------------------------------------ segment lanes (r1g)
 // One wave per capture, blocks of 64 x SEG bytes: lane j owns the SEG bytes
@@ -914,6 +852,10 @@ crc32_search_o_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restr
   }
 }
 
+#ifdef LNX_RESEARCH
+#include "research/search_research.inc"
+#endif
+
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream) {
   if (n == 0) return hipSuccess;
@@ -926,127 +868,11 @@ hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const 
 #ifndef LNX_RESEARCH
   // product: octet segments, 8 captures per wave (r4)
   launch_octets();
-#else
-  // research library:
-  // LNX_PROF_SEARCH=word selects the word-lane kernel
-  // LNX_PROF_SEARCH=h selects the per-lane hit bitmask pass B, =6 pass A all by Z_4,
-  // =s the 24-byte-segment kernel (one capture per wave, the r1h product);
-  // LNX_PROF_SEARCH_ZWORDS=0|2|4|8|10 the two-capture kernel's pass A split
-  static const char mode = [] {
-    const char* e = getenv("LNX_PROF_SEARCH");
-    return e ? e[0] : '\0';
-  }();
-  if (mode == 'w') {
-    uint64_t grid = (n + 3) / 4;
-    const uint64_t cap = (uint64_t)num_cus * 8;
-    if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(crc32_search_kernel, dim3((unsigned)grid), dim3(kSearchBlock), 0, stream, bytes, off,
-                       min_off, n, tables, result);
-  } else {
-    uint64_t grid = (n + kSegBlock / 64 - 1) / (kSegBlock / 64);
-    const uint64_t cap = (uint64_t)num_cus * 2;
-    if (grid > cap) grid = cap;
-    if (mode == 'h')  // per-lane hit bitmask, pass A all Z_4 (r1h before the ballot form)
-      hipLaunchKernelGGL((crc32_search_seg_kernel<false, 6>), dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes,
-                         off, min_off, n, tables, result);
-    else if (mode == '6')  // pass A all Z_4
-      hipLaunchKernelGGL((crc32_search_seg_kernel<true, 6>), dim3((unsigned)grid), dim3(kSegBlock), 0, stream, bytes,
-                         off, min_off, n, tables, result);
-    else if (mode == 's')  // 24-byte segments, one capture per wave (the r1h product)
-      hipLaunchKernelGGL((crc32_search_seg_kernel<true, kSearchZWords>), dim3((unsigned)grid), dim3(kSegBlock), 0,
-                         stream, bytes, off, min_off, n, tables, result);
-    else {  // two captures per wave, 48-byte segments
-      static const int zw = [] {
-        const char* e = getenv("LNX_PROF_SEARCH_ZWORDS");
-        return e ? atoi(e) : -1;
-      }();
-      uint64_t g2 = ((n + 1) / 2 + kSegBlock / 64 - 1) / (kSegBlock / 64);
-      if (g2 > cap) g2 = cap;
-      if (mode != '0' && zw == 0)
-        hipLaunchKernelGGL((crc32_search_half_kernel<0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode != '0' && zw == 8)
-        hipLaunchKernelGGL((crc32_search_half_kernel<8>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode != '0' && zw == 2)
-        hipLaunchKernelGGL((crc32_search_half_kernel<2>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode != '0' && zw == 10)
-        hipLaunchKernelGGL((crc32_search_half_kernel<10>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode != '0' && zw == 4)
-        hipLaunchKernelGGL((crc32_search_half_kernel<4>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode == 'b')  // r2 byte-chain pass B (pass A all by Z_4)
-        hipLaunchKernelGGL((crc32_search_half_kernel<12>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      else if (mode == '0' && zw == 8)  // word checks with byte-chain steps, pass A 8 of 12 words by Z_4
-        hipLaunchKernelGGL((crc32_search_half_kernel<8, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '0' && zw == 6)
-        hipLaunchKernelGGL((crc32_search_half_kernel<6, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '0' && zw == 4)
-        hipLaunchKernelGGL((crc32_search_half_kernel<4, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '0' && zw == 10)
-        hipLaunchKernelGGL((crc32_search_half_kernel<10, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '0')  // word checks, pass B's Z_4 steps all as byte chains
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == 'n')  // word checks, pass B's Z_4 steps by lane-private nibble tables
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, -1>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '2')  // word checks, 2 of 11 pass-B steps by Z_4
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 2>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '4')  // word checks, 4 of 11 pass-B steps by the shared Z_4 tables
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 4>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == '8')  // word checks, 8 of 11 by Z_4
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 8>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == 'z')  // word checks, every pass-B step by the shared Z_4 tables (bank conflicts)
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 12>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == 'x')  // word checks with byte-chain Z_4 steps, shared Z_4 in pass A, 2 blocks per CU (r2s2d)
-        hipLaunchKernelGGL((crc32_search_half_kernel<12, true, 0>), dim3((unsigned)g2), dim3(kSegBlock), 0, stream,
-                           bytes, off, min_off, n, tables, result);
-      else if (mode == 'u') {  // the U layout with one capture per half (r2s2e)
-        const uint64_t g1 = g2 < (uint64_t)num_cus ? g2 : (uint64_t)num_cus;
-        hipLaunchKernelGGL(crc32_search_u_kernel<0>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
-                           min_off, n, tables, result);
-      } else if (mode == '1') {  // U layout, one capture per half, each segment as two 24-byte chains
-        const uint64_t g1 = g2 < (uint64_t)num_cus ? g2 : (uint64_t)num_cus;
-        hipLaunchKernelGGL((crc32_search_u_kernel<1, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      } else if (mode == 'g' || mode == 'G') {  // product with the guarded global loads (g) / unmerged group loads (G)
-        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
-        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-        if (mode == 'g')
-          hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 0>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
-                             bytes, off, min_off, n, tables, result);
-        else
-          hipLaunchKernelGGL((crc32_search_u_kernel<2, false, 2>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream,
-                             bytes, off, min_off, n, tables, result);
-      } else if (mode == 'U') {  // the r2 / r3 product: four captures per wave, 48-byte segments
-        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
-        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-        hipLaunchKernelGGL(crc32_search_u_kernel<2>, dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes, off,
-                           min_off, n, tables, result);
-      } else if (mode == 'q') {  // U layout, two captures per half, each segment as two 24-byte chains
-        uint64_t g1 = ((n + 3) / 4 + kSegBlock / 64 - 1) / (kSegBlock / 64);
-        if (g1 > (uint64_t)num_cus) g1 = (uint64_t)num_cus;
-        hipLaunchKernelGGL((crc32_search_u_kernel<2, true>), dim3((unsigned)g1), dim3(kSegBlock), 0, stream, bytes,
-                           off, min_off, n, tables, result);
-      } else {  // the product (octet segments)
-        launch_octets();
-      }
-    }
-  }
-#endif  // LNX_RESEARCH
   return hipGetLastError();
+#else
+  (void)launch_octets;
+  return launch_crc32_search_research(bytes, off, min_off, n, tables, result, num_cus, stream);
+#endif
 }
 
 }  // namespace lnx

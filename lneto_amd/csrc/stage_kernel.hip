@@ -525,7 +525,11 @@ template <StageMode MODE>
 __global__ void __launch_bounds__(kStageW * 64, 1)
 crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t nframes,
                    uint64_t frames_per_wg, const uint32_t* __restrict__ image, void* __restrict__ out,
-                   uint32_t policy, uint32_t* __restrict__ scratch) {
+                   uint32_t policy, uint32_t* __restrict__ scratch, const uint32_t* __restrict__ stage_flag,
+                   uint32_t epoch) {
+  // behind the rows launch (the plain entries): nothing to do unless one of
+  // its workgroups found a slice for this kernel (one word, this call's epoch)
+  if (stage_flag && *stage_flag != epoch) return;
   constexpr uint32_t kLast = kStageBF + 1;  // the list's last entry (a sentinel past bf)
   constexpr uint32_t kThreads = kStageW * 64;
   __shared__ __attribute__((aligned(16))) char lds[kSBytes];
@@ -879,7 +883,8 @@ crc32_stage_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 }
 
 hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_t n, void* out, bool verify,
-                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream) {
+                              uint32_t policy, const void* image, uint32_t* scratch, int num_cus, hipStream_t stream,
+                              const uint32_t* stage_flag, uint32_t epoch) {
   if (n == 0) return hipSuccess;
   const SlicePlan pl = slice_plan(n, num_cus);
   const uint32_t* img = static_cast<const uint32_t*>(image);
@@ -889,10 +894,10 @@ hipError_t launch_crc32_stage(const uint8_t* bytes, const uint64_t* off, uint64_
   const unsigned grid = (unsigned)(pl.grid > (uint64_t)num_cus ? pl.grid : (uint64_t)num_cus);
   if (verify)
     hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kVerify>, dim3(grid), dim3(kStageW * 64), 0, stream, bytes, off,
-                       n, pl.per, img, out, policy, scratch);
+                       n, pl.per, img, out, policy, scratch, stage_flag, epoch);
   else
     hipLaunchKernelGGL(crc32_stage_kernel<StageMode::kCrc>, dim3(grid), dim3(kStageW * 64), 0, stream, bytes, off, n,
-                       pl.per, img, out, policy, scratch);
+                       pl.per, img, out, policy, scratch, stage_flag, epoch);
   return hipGetLastError();
 }
 

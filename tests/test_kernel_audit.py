@@ -45,7 +45,7 @@ def test_no_divergent_exit_loop_around_wide_loads(tmp_path, src, build):
     """tools/prof/audit_loops.py over every product kernel: no innermost loop
     that retires lanes with s_andn2_b64 exec and issues multi-dword loads (the
     shape of round 1's wrong-sum sum16 form)."""
-    path = os.path.join(ROOT, "lneto_amd", "csrc", src + ".hip")
+    path = os.path.join(ROOT, "lneto_amd", "csrc", ("research/" if src == "stage_research" else "") + src + ".hip")
     flags = ["-DLNX_RESEARCH"] if build == "research" else []
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-mllvm",
                     "-amdgpu-atomic-optimizer-strategy=None", "-c", "--save-temps", *flags, "-o", str(tmp_path / "k.o"),
@@ -73,7 +73,7 @@ def test_stage_kernel_passes_the_ring_audit(tmp_path, src, nsyms):
     vmcnt(10) must cover the 8 loads of the slot it drains, with the
     held-result stores (2 per round, in asm so hipcc cannot drop or move them)
     and the next slot's 8 loads younger than it."""
-    path = os.path.join(ROOT, "lneto_amd", "csrc", src + ".hip")
+    path = os.path.join(ROOT, "lneto_amd", "csrc", ("research/" if src == "stage_research" else "") + src + ".hip")
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++20", "-c", "--save-temps", "-DLNX_RESEARCH",
                     "-o", str(tmp_path / "k.o"), path], cwd=tmp_path, check=True, capture_output=True)
     asm = next(p for p in os.listdir(tmp_path) if p.endswith("gfx950.s"))
