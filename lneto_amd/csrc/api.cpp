@@ -819,19 +819,22 @@ int lnx_device_count(void) {
 const char* lnx_last_error(void) { return g_last_error.c_str(); }
 
 const char* lnx_version(void) {
-  return "lneto_amd 0.11 gfx950: crc32 rows (32-lane whole-line rows from 4096 B mean: 24-line items; one-word "
+  return "lneto_amd 0.12 gfx950: crc32 rows (32-lane whole-line rows from 4096 B mean: 24-line items; one-word "
          "16-lane rows 1600-4096 B: 1 slot x 24 steps, 4-frame chunks; lean two-word line rows 640-1600 B, offsets "
          "and segment mode: one 13-line frame per row per slot; whole-line rows load a frame's first and last lines "
          "at the default cache policy, the rest nt; 4-lane rows: 2 slots x 16 steps, 32-frame chunks, held results; "
          "narrow rows load only the 4-step runs an item has; TX FCS append in the same launch: pad, FCS, length, "
-         "status) + sum16 16-lane line rows + ingress verdicts (qword rows, end mask on the last qword, ICMP "
-         "clients' checks) and TX checksum generate (the same rows, GEN) + rx ring (ingress and egress packets) + "
-         "CRC32Search (eight captures per wave, 192-byte lane segments as four 48-byte chains joined by "
-         "lane-private Z_48 nibble tables, 3-level scan, Z_4 in the lane-private U layout, pass B by word checks, "
-         "group-descriptor loads) + staged lane streams for short-frame batches (slicing-by-8 fold, LDS transposed "
-         "whole-line loads) and slice dispatch on the device + rx_verify (FCS and verdicts in one read: 16-lane "
-         "rows, 48-frame groups, the next pass loaded ahead) + tx_finish (checksums, padding and FCS in one read, "
-         "CRC corrected by linearity; 12 waves) + zero copy through the ring's pinned slots";
+         "status; segment slices out of address order folded frame by frame) + sum16 16-lane line rows + ingress "
+         "verdicts (qword rows, end mask on the last qword, ICMP clients' checks) and TX checksum generate (the same "
+         "rows, GEN) + rx ring (ingress and egress packets) + CRC32Search (eight captures per wave, 192-byte lane "
+         "segments as four 48-byte chains joined by lane-private Z_48 nibble tables, 3-level scan, Z_4 in the "
+         "lane-private U layout, pass B by word checks, group-descriptor loads) + staged lane streams for "
+         "short-frame batches (slicing-by-8 fold, LDS transposed whole-line loads; out-of-order blocks by lane and "
+         "by whole waves) and slice dispatch on the device (staged launch gated by the rows launch's flag word; "
+         "giant slices by span, mean or 8x skew, out-of-order giant slices frame by frame) + rx_verify (FCS and "
+         "verdicts in one read: 16-lane rows, 56-frame groups, the next pass loaded ahead, units no frame reaches "
+         "skipped) + tx_finish (checksums, padding and FCS in one read, CRC corrected by linearity; 16 waves, "
+         "48-frame groups) + zero copy through the ring's pinned slots";
 }
 
 }  // extern "C"

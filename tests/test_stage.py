@@ -432,3 +432,34 @@ def test_gpu_large_frames_among_zipf(cuda, mode):
     assert ms <= 10.0, ts
     del d, o, c
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_gpu_frame_past_4gib(cuda):
+    """One 4.5 GB frame (positions inside it past 2^32) between short ones:
+    the giant pieces' 64-bit positions and Z_d shifts for d up to 2^33 (the
+    HBM image's nibble tables m = 31..39), CRC through both entries against the
+    C oracle, then its FCS appended verifies and a flipped byte past 2^32 fails it."""
+    import torch
+    from lneto_amd import synth
+    from oracle import oracle as O
+    big = 4_500_000_000
+    lens = np.array([100, 7, big, 1500, 0, 64], dtype=np.int64)
+    off = (synth.offsets_from_lengths(lens) + 9).astype(np.uint64)
+    d = synth.bytes_torch(int(off[-1]) + 8, cuda, seed=97)
+    host = d.cpu().numpy()
+    want = O.crc32_frames(host, off, threads=8, amd64=O.has_clmul())
+    for mode in MODES:
+        got = _run(cuda, d, off, mode)
+        assert (got == want).all(), (mode, got, want)
+    s, e = int(off[2]), int(off[3])
+    fcs = int(O.crc32_frames(host, np.array([s, e - 4], np.uint64), amd64=O.has_clmul())[0])
+    del host
+    d[e - 4:e] = torch.tensor(list(fcs.to_bytes(4, "little")), dtype=torch.uint8, device=cuda)
+    for mode in MODES:
+        assert _run(cuda, d, off, mode, verify=True)[2] == 1, mode
+    d[s + (1 << 32) + 12345] ^= 4
+    for mode in MODES:
+        assert _run(cuda, d, off, mode, verify=True)[2] == 0, mode
+    del d
+    torch.cuda.empty_cache()
