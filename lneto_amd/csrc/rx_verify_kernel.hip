@@ -223,10 +223,40 @@ __device__ uint2 g_rv_zero[2];
 // memory, read over PCIe): the qwords past the frame's end are captured as the
 // fold passes them instead of loaded again (a second PCIe round trip).
 template <bool CRC, bool TX, bool HOST, int PF = kRvPf>
-__device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head, const RvLane& z, const uint8_t* bytes,
-                                        uint64_t sk, uint32_t Ltk, uint32_t nrow, uint32_t trim, uint32_t capacity) {
+__device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* head, const RvLane& z,
+                                            const uint8_t* bytes, uint64_t sk, uint32_t Ltk, uint32_t nrow,
+                                            uint32_t trim, uint32_t capacity) {
   const uint32_t lane = threadIdx.x & 63u, p = lane & 15u, row = lane >> 4;
   const uint2* zero = g_rv_zero;
+    // The passes take the group's frames in order of their length class (128-B
+    // lines): a pass folds as many units as its longest frame needs, so four
+    // frames of like length waste fewer of them on a mixed batch.  A counting
+    // sort over the classes (stable; lanes past nrow stay last) gives each
+    // lane its position `rank`, and the frames' starts and lengths move there
+    // (ds_permute), so the passes below take position k = 4 j + row as
+    // before and leave the frame's results at res[rank] / head[rank]: the
+    // caller's lane-per-frame phase reads its frame there.  A uniform group
+    // (MTU frames) skips the sort (rank = lane).
+    uint32_t rank = lane;
+    {
+      const uint32_t key = lane < nrow ? ((Ltk + 127u) >> 7 < 14u ? (Ltk + 127u) >> 7 : 14u) : 15u;
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+      if (__builtin_amdgcn_ballot_w64(lane < nrow && key != k0) != 0) {
+        uint32_t below = 0;
+        uint64_t same = 0;
+#pragma unroll 1
+        for (uint32_t c = 0; c < 16u; ++c) {
+          const uint64_t m = __builtin_amdgcn_ballot_w64(key == c);
+          below += key > c ? (uint32_t)__builtin_popcountll(m) : 0u;
+          same = key == c ? m : same;
+        }
+        rank = below + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
+        const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)(uint32_t)sk);
+        const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)(uint32_t)(sk >> 32));
+        Ltk = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)Ltk);
+        sk = ((uint64_t)shi << 32) | slo;
+      }
+    }
     // the row's frame of pass j: its start (from the lane that holds it) and length
     auto row_frame = [&](uint32_t j, const uint8_t*& fr, uint32_t& Lt) {
       const uint32_t k = 4u * j + row;
@@ -286,7 +316,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
 #pragma unroll
     for (int a = 0; a < PR; ++a) prefetch(a, (uint32_t)a);
     for (uint32_t j = 0; 4u * j < nrow; ++j) {
-      const uint32_t k = 4u * j + row;  // the row's frame in the group
+      const uint32_t k = 4u * j + row;  // the row's frame in the group (its sorted position)
       const uint8_t* fr = frn[0];
       // Lt: the bytes loaded and folded; Lc: the CRC's length (zeros past Lt); L: the sum's end
       const uint32_t Lt = Ltn[0];
@@ -413,6 +443,7 @@ __device__ __forceinline__ void rv_rows(const char* lds, uint2* res, uint2* head
       S = rv_row_add(S);
       if (p == 0) res[k] = make_uint2(okf, S);
     }
+    return rank;
 }
 
 template <bool CRC, bool FILT, bool HOST>
@@ -441,7 +472,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     __syncthreads();
   }
   const uint32_t trim = CRC ? 4u : 0u;
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u, wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const RvLane z(lane);
   uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (FCS ok, S) per frame
   uint2* head = res + kRvGroup;                                                // kRvHead qwords per frame
@@ -463,7 +494,9 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     // ---------------------------------------------------------------- A: data
     // (the whole next pass loaded ahead from HBM: 0.335 against 0.340-0.344 ms for 8 of
     // its 12 qwords; over PCIe 8 measured 34.4 against 33.7 GiB/s)
-    rv_rows<CRC, false, HOST, HOST ? kRvPf : kRvPfRx>(lds, res, head, z, bytes, sk, Ltk, nrow, trim, 0u);
+    // (the frame's results sit at its position in the passes' order: pos)
+    const uint32_t pos = rv_rows<CRC, false, HOST, HOST ? kRvPf : kRvPfRx>(lds, res, head, z, bytes, sk, Ltk, nrow, trim,
+                                                                           0u);
     __builtin_amdgcn_wave_barrier();  // (the wave's own LDS writes, read back in order below)
 
     // ---------------------------------------------------------------- B: verdicts
@@ -474,7 +507,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((Lt + mis + 7u) >> 3);
-    const uint32_t kk = lane < gsz ? lane : 0u;
+    const uint32_t kk = lane < gsz ? pos : 0u;
     // the staged qwords 0 .. kRvHead - 1 of the frame's window (frame offsets -mis .. 72 - mis),
     // then qwords 9, 10 from memory for the frames that need them (IPv4 options past offset 64)
     uint32_t dw[22];
@@ -814,7 +847,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     for (uint32_t i = t; i < 16u * 128u; i += kB) reinterpret_cast<uint32_t*>(lds + kTxP)[i] = image[kTxImgP + i];
     __syncthreads();
   }
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u, wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const RvLane z(lane);
   uint2* res = reinterpret_cast<uint2*>(lds + kTabBytes + kWaveBytes * wv);  // (R0, S) per frame
   uint2* head = res + kTxGroup;
@@ -830,7 +863,8 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint64_t sk = start[fi];
     const uint32_t Ltk = live ? len[fi] : 0u;
     const uint32_t nrow = (uint32_t)(n - g * gsz < gsz ? n - g * gsz : gsz);
-    rv_rows<FCS, true, HOST, HOST ? kRvPf : kTxPf>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u, capacity);
+    const uint32_t pos = rv_rows<FCS, true, HOST, HOST ? kRvPf : kTxPf>(lds, res, head, z, bytes, sk, Ltk, nrow, 0u,
+                                                                         capacity);
     __builtin_amdgcn_wave_barrier();
 
     // ---------------------------------------------------------------- B: one lane per frame
@@ -839,7 +873,7 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 7u);
     const uint2* base2 = reinterpret_cast<const uint2*>(fr - mis);
     const int32_t QE = (int32_t)((L + mis + 7u) >> 3);
-    const uint32_t kk = lane < gsz ? lane : 0u;
+    const uint32_t kk = lane < gsz ? pos : 0u;
     // the staged window bytes, read from LDS where used (held in registers, the
     // header words cost the kernel its occupancy: see kTxBlock); qwords 9 and 10
     // (IPv4 options past the staged bytes) from memory below

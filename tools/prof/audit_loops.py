@@ -174,6 +174,12 @@ def vgpr_writes(body, dep):
         mn, ops = operands(l)
         if not ops:
             continue
+        if mn == "v_writelane_b32":
+            # writes its one lane whatever exec is (hipcc's SGPR spill slots:
+            # v_writelane under a narrowed exec, v_readlane later): depth 0
+            for r in regs_of(ops[0]):
+                out.append((i, r, 0))
+            continue
         if (re.match(r"^(v_|ds_read|ds_bpermute|ds_swizzle|global_load|buffer_load|flat_load|scratch_load)", mn)
                 or re.match(r"^(global_atomic|buffer_atomic|ds_)\w*_rtn", mn)) and not mn.startswith(
                     ("v_cmp", "v_readfirstlane", "v_readlane")):
