@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of two builds of the library on one box: bench.py runs alternately
 under LNETO_AMD_LIB=A and =B (separate processes, same arguments), REPS times
-each; prints every line's kernel time and the medians.
+each; prints every line's kernel time (the host clock per step for the
+host-memory ops) and the medians.
 
 usage: lib_ab.py LIB_A LIB_B REPS [bench.py args ...]"""
 import json
@@ -22,8 +23,9 @@ for r in range(reps):
             print(out.stdout[-2000:], out.stderr[-2000:])
             sys.exit(1)
         d = json.loads(line[-1])
-        res[lib].append(d["roofline"]["kernel_ms"])
-        print(f"{os.path.basename(lib):28s} kernel_ms {d['roofline']['kernel_ms']:.4f} frac {d['roofline']['frac']:.4f}",
-              flush=True)
+        r = d.get("roofline") or {}
+        ms = r.get("kernel_ms", d["ms_per_step"])  # (host-memory ops: the host clock per step)
+        res[lib].append(ms)
+        print(f"{os.path.basename(lib):28s} ms {ms:.4f} frac {r.get('frac', 0):.4f} value {d['value']}", flush=True)
 for lib, v in res.items():
     print(f"median {os.path.basename(lib):28s} {statistics.median(v):.4f} ms  ({' '.join(f'{x:.4f}' for x in v)})")
