@@ -338,15 +338,27 @@ __device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* im
   __syncthreads();
   {
     const uint32_t TF = gpre[G];
-    for (uint32_t t0 = 0; t0 < TF; t0 += kStageW * 64u) {
-      const uint32_t t = t0 + threadIdx.x;
-      uint32_t g = 0;
-      for (uint32_t step = 256u; step > 0; step >>= 1)
-        if (g + step <= G && gpre[g + step] <= t) g += step;
-      if (t < TF) {
-        const uint64_t i = (uint64_t)g * per + (t - gpre[g]);
-        if (off[i + 1] < off[i]) __hip_atomic_fetch_or(badm + (g >> 5), 1u << (g & 31u), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    // four pairs a thread per step, their loads in flight together
+    for (uint32_t t0 = 0; t0 < TF; t0 += 4u * kStageW * 64u) {
+      uint64_t i[4];
+      uint32_t g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t t = t0 + (uint32_t)u * kStageW * 64u + threadIdx.x;
+        uint32_t gg = 0;
+        for (uint32_t step = 256u; step > 0; step >>= 1)
+          if (gg + step <= G && gpre[gg + step] <= t) gg += step;
+        g[u] = gg;
+        i[u] = t < TF ? (uint64_t)gg * per + (t - gpre[gg]) : 0u;  // (t past TF: pair 0, 1, never flagged below)
+      }
+      uint64_t a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = off[i[u]], b[u] = off[i[u] + 1];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t t = t0 + (uint32_t)u * kStageW * 64u + threadIdx.x;
+        if (t < TF && b[u] < a[u])
+          __hip_atomic_fetch_or(badm + (g[u] >> 5), 1u << (g[u] & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
   }
@@ -421,30 +433,53 @@ __device__ __forceinline__ void giant_pieces(const char* lds, const uint32_t* im
     uint64_t cur = cross_in ? lb - 1 : lb;
     uint64_t scur = cross_in ? off[lb - 1] : olb;
     uint64_t x = cur < F1 ? off[cur + 1] : ~0ull;  // the current frame's end
+    // the next frame's end, loaded one advance ahead: an advance takes it and
+    // issues the load of the one after, whose value is first read at the
+    // lane's next advance (in the byte-serial blocks a lane's frame ends are
+    // ~a frame apart; waiting for the load at every end event of every lane
+    // made a 16 KiB piece of Zipf frames cost milliseconds)
+    uint64_t xn = off[cur + 2u <= F1 ? cur + 2u : F1];
     uint32_t r = cross_in ? 0u : 0xFFFFFFFFu;
     // a frame's end event (its end at `at`): finish it here when all of it lies
     // in the piece, else add this piece's part
+    // (every lane calls it, ev per lane).  The parts a wave's lanes add to
+    // one frame (consecutive pieces of a long frame: up to 64 a wave) are
+    // XORed across the wave first and added by one lane with their count, so
+    // the slot of a 2 GB frame takes ~2 K atomics rather than 134 K
+    // (same-address device atomics serialize at ~12 ns)
     auto frame_end = [&](bool ev, uint64_t at) {
       const bool here = scur >= a && at <= b;
       if (ev && here) stage_store<MODE>(out, cur, stage_value<MODE>(r, at - scur));
-      if (ev && !here) {
-        const uint32_t slot = pre[g] + (uint32_t)((scur - S) / P) + 1u;
-        const uint32_t nparts = (uint32_t)((at - 1u - S) / P - (scur - S) / P + 1u);
-        __hip_atomic_fetch_xor(acc + slot, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t old = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1u == nparts) {
-          const uint32_t tot = __hip_atomic_exchange(acc + slot, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          stage_store<MODE>(out, cur, stage_value<MODE>(tot, at - scur));
+      const bool part = ev && !here;
+      const uint32_t slot = part ? pre[g] + (uint32_t)((scur - S) / P) + 1u : 0u;
+      for (uint64_t pend = __builtin_amdgcn_ballot_w64(part); pend != 0;) {
+        const uint32_t l0 = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)slot, (int)l0);
+        const bool mine = part && slot == s0;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(mine);
+        uint32_t v = mine ? r : 0u;
+#pragma unroll
+        for (int sft = 1; sft < 64; sft <<= 1) v ^= (uint32_t)__shfl_xor((int)v, sft);
+        if (lane == l0) {
+          const uint32_t np = (uint32_t)__builtin_popcountll(m);
+          const uint32_t nparts = (uint32_t)((at - 1u - S) / P - (scur - S) / P + 1u);
+          __hip_atomic_fetch_xor(acc + s0, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t old = __hip_atomic_fetch_add(cnt + s0, np, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+          if (old + np == nparts) {
+            const uint32_t tot = __hip_atomic_exchange(acc + s0, 0u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cnt + s0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stage_store<MODE>(out, cur, stage_value<MODE>(tot, at - scur));
+          }
         }
+        pend &= ~m;
       }
     };
     auto advance = [&](bool ev) {
-      const uint64_t nx = off[cur + 2u <= F1 ? cur + 2u : F1];  // (loaded by every lane)
       cur = ev ? cur + 1u : cur;
       scur = ev ? x : scur;
       r = ev ? 0xFFFFFFFFu : r;
-      x = ev ? (cur < F1 ? nx : ~0ull) : x;
+      x = ev ? (cur < F1 ? xn : ~0ull) : x;
+      xn = off[cur + 2u <= F1 ? cur + 2u : F1];  // (every lane, unconditionally: no select waits on it)
     };
     // 128-byte blocks from the line holding a
     const uint64_t blk0 = a - ((reinterpret_cast<uintptr_t>(bytes) + a) & 127u);
