@@ -218,7 +218,7 @@ int lnx_sum16_batch(const uint8_t* d_bytes, const uint64_t* d_off, const uint32_
 int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const int64_t* d_min_off, uint64_t n,
                            int64_t* d_result, void* stream);
 
-/* Receive-path checksum verdicts, one fused kernel: for
+/* Receive-path checksum verdicts, fused kernels: for
  * every Ethernet frame d_bytes[d_off[i] : d_off[i+1]] (FCS already stripped)
  * d_verdict[i] = the result lneto's receive path reaches at its checksum
  * stage — StackEthernet.Demux size checks (internet/stack-ethernet.go:139-165),
@@ -232,7 +232,11 @@ int lnx_crc32_search_batch(const uint8_t* d_bytes, const uint64_t* d_off, const 
  * 18 ErrTruncatedFrame.  Destination filtering and handler lookup are stack
  * configuration and are taken as accept-all.  With LNX_VERIFY_ICMP, ICMP
  * messages also take their client's Demux checks up to the checksum
- * (ipv4/icmpv4/client.go:89-102, ipv6/icmpv6/client.go:100-115). */
+ * (ipv4/icmpv4/client.go:89-102, ipv6/icmpv6/client.go:100-115).  Two
+ * launches, one of which works: the ingress rows, or for a batch whose mean
+ * frame is under 1280 B the receive check's rows without the CRC (the same
+ * verdicts; the choice is made on the device from d_off[0] and d_off[n], with
+ * a word of the stream's scratch, as lnx_crc32_batch). */
 int lnx_ingress_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                              uint8_t* d_verdict, void* stream);
 

@@ -36,10 +36,12 @@ hipError_t launch_fcs_scatter(uint8_t* bytes, const uint64_t* start, uint32_t* l
 #endif
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false);
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false,
+                            const uint32_t* gate = nullptr, uint32_t epoch = 0);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
-                                 uint32_t trim, const RxFilter* filter);
+                                 uint32_t trim, const RxFilter* filter, uint32_t* gate = nullptr, uint32_t epoch = 0,
+                                 uint64_t short_mean = 0);
 hipError_t launch_crc32_search(const uint8_t* bytes, const uint64_t* off, const int64_t* min_off, uint64_t n,
                                const uint32_t* tables, int64_t* result, int num_cus, hipStream_t stream);
 hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
@@ -376,7 +378,11 @@ int get_ctx(DeviceCtx** out) {
 // no reset)
 constexpr size_t kGiantSlots = (1u << 20) + 4096u;
 constexpr size_t kStageFlag = 2 * kGiantSlots;
+constexpr size_t kIngressGate = kStageFlag + 1;  // lnx_ingress_verify_batch's second launch (the same epoch rule)
 constexpr size_t kScratchWords = kStageFlag + 16;
+// the mean frame length from which the ingress rows beat the receive check
+// without its CRC (tools/prof/ingress_vs_rv.py)
+constexpr uint64_t kIngressShortMean = 1280;
 
 // The calling device's giant-slice scratch for `stream`, zeroed on that
 // stream when made (stream order puts the zeroing before the first launch).
@@ -638,9 +644,22 @@ int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_ingress_verify(d_bytes, d_off, n, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP), d_verdict,
-                                       c->num_cus, static_cast<hipStream_t>(stream), nullptr, 0, &filt);
+  // two launches, one of which works (the mean frame length is device-resident):
+  // the ingress rows for a batch whose mean frame is >= kIngressShortMean
+  // bytes, else the receive check without its CRC (rx_verify_kernel: the same
+  // verdicts, no ok output), gated by a word of the stream's scratch
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  uint32_t* scratch = nullptr;
+  uint32_t epoch = 0;
+  if ((st = giant_scratch(c, hs, &scratch, &epoch)) != LNX_OK) return st;
+  uint32_t* gate = scratch + kIngressGate;
+  const uint32_t vf = flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP);
+  hipError_t e = launch_ingress_verify(d_bytes, d_off, n, vf, d_verdict, c->num_cus, hs, nullptr, 0, &filt, gate, epoch,
+                                       kIngressShortMean);
   if (e != hipSuccess) return hip_fail(e, "ingress_verify_kernel launch");
+  e = launch_rx_verify(d_bytes, d_off, n, vf, false, nullptr, d_verdict, nullptr, &filt, c->d_rx, c->num_cus, hs, false,
+                       gate, epoch);
+  if (e != hipSuccess) return hip_fail(e, "rx_verify_kernel launch");
   return LNX_OK;
 }
 

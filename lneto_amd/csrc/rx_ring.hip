@@ -56,7 +56,8 @@ namespace lnx {
 int device_resources(const void** image, int* num_cus, const void** stage_image, const void** rx_image);
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false);
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host = false,
+                            const uint32_t* gate = nullptr, uint32_t epoch = 0);
 int hip_error(hipError_t e, const char* what);
 // host_path.cpp: the per-frame host forms (batches below the ring's host threshold)
 uint8_t host_verdict(const uint8_t* fr, size_t L, uint32_t flags, const RxFilter& f);
@@ -67,7 +68,8 @@ hipError_t launch_fcs_verify_segments(const uint8_t* bytes, const uint64_t* star
                                       uint8_t* ok, const void* images, int num_cus, hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
-                                 uint32_t trim, const RxFilter* filter);
+                                 uint32_t trim, const RxFilter* filter, uint32_t* gate = nullptr, uint32_t epoch = 0,
+                                 uint64_t short_mean = 0);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
                               uint8_t* status, int num_cus, hipStream_t stream);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,

@@ -452,7 +452,12 @@ template <bool CRC, bool FILT, bool HOST>
 __global__ void __launch_bounds__(kRvBlock)
 rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n, uint32_t flags,
                  uint8_t* __restrict__ okv, uint8_t* __restrict__ verdict, const uint32_t* __restrict__ seg_len,
-                 const uint32_t* __restrict__ image, uint32_t gsz, RxFilter filt) {
+                 const uint32_t* __restrict__ image, uint32_t gsz, RxFilter filt, const uint32_t* __restrict__ gate,
+                 uint32_t epoch) {
+  // behind the ingress launch (lnx_ingress_verify_batch on a short-frame
+  // batch, launch_ingress_verify): nothing to do unless it left this call's
+  // epoch in the gate word
+  if (gate && *gate != epoch) return;
   constexpr uint32_t kTabBytes = CRC ? kRvBytes : 0u;
   constexpr uint32_t kWaveBytes = kRvGroup * 8u * (1u + kRvHead);
   __shared__ __attribute__((aligned(16))) char lds[kTabBytes + (kRvBlock / 64) * kWaveBytes];
@@ -738,7 +743,7 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     if (v == 0) v = v_udp4;  // udp.NewFrame / ValidateSize follow CalculateHeaderCRC (stack-ip4.go:128-159)
     if (v == 0 && l4_sum && rv_sum16(tX + lseed) != 0) v = kErrBadCRC;
     if (live) {
-      okv[f] = (uint8_t)rk.x;
+      if (okv) okv[f] = (uint8_t)rk.x;  // (null: the verdicts alone, for lnx_ingress_verify_batch)
       verdict[f] = (uint8_t)v;
     }
     __builtin_amdgcn_wave_barrier();  // the next group rewrites res and head
@@ -1153,7 +1158,8 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
 
 hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags, bool fcs,
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
-                            const uint32_t* image, int num_cus, hipStream_t stream, bool host) {
+                            const uint32_t* image, int num_cus, hipStream_t stream, bool host, const uint32_t* gate,
+                            uint32_t epoch) {
   RxFilter filt{};
   if (filter) filt = *filter;
   if (n == 0) return hipSuccess;
@@ -1162,7 +1168,7 @@ hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t 
   const uint32_t gsz = balanced_group(n, grid * (kRvBlock / 64), kRvGroup);
 #define LNX_RV(C, F, H)                                                                                       \
   hipLaunchKernelGGL((rx_verify_kernel<C, F, H>), dim3((unsigned)grid), dim3(kRvBlock), 0, stream, bytes, off, n, \
-                     flags, ok, verdict, seg_len, image, gsz, filt)
+                     flags, ok, verdict, seg_len, image, gsz, filt, gate, epoch)
   if (host) {
     if (fcs) {
       if (filt.on) LNX_RV(true, true, true); else LNX_RV(true, false, true);

@@ -292,3 +292,38 @@ def test_gpu_icmp_verdicts_match_oracle(cuda, base_pad, flags):
     want = np.array([O.ingress_verdict(f, flags) for f in frames], dtype=np.uint8)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", ["rx_verify", "ingress_rows"])
+@pytest.mark.parametrize("filt", [None, "plain", "few_handlers"])
+@pytest.mark.parametrize("flags", [0, 3])
+def test_gpu_ingress_both_routes(cuda, route, filt, flags):
+    """lnx_ingress_verify_batch launches the ingress rows and the receive check
+    without its CRC (rx_verify_kernel), and the one the batch's mean frame
+    length picks works (api.cpp kIngressShortMean, 1280 B): the generator's,
+    the ICMP and the filter frames alone (mean ~100 B: the receive check) and
+    with long valid frames after them so that the mean passes 1280 B (the
+    ingress rows), both against the oracle, with and without a stack filter."""
+    import torch
+    import lneto_amd as L
+    from tests.test_rx_filter import _pair
+    frames = G.frames(seed=91, count=1500) + G.icmp_frames(seed=92, count=400) + G.filter_frames(seed=93, count=600)
+    if route == "ingress_rows":
+        rng = np.random.default_rng(94)
+        need = 1280 * len(frames) - sum(len(f) for f in frames)
+        while need > -1280 * (len(frames) + 1):  # (the mean past the threshold with margin)
+            pay = rng.integers(0, 256, size=int(rng.integers(7000, 8900)), dtype=np.uint8).tobytes()
+            f = G.ether(0x0800, G.ipv4(17, G.udp(pay))) if len(frames) % 2 else G.ether(0x86DD, G.ipv6(6, G.tcp(pay)))
+            frames.append(f)
+            need += 1280 - len(f)
+    mean = sum(len(f) for f in frames) / len(frames)
+    assert (mean >= 1280) == (route == "ingress_rows")
+    of, lf = _pair(filt) if filt else (None, None)
+    data, off = _pack(frames, 3)
+    got = L.ingress_verify_batch(torch.from_numpy(data).to(cuda), torch.from_numpy(off.astype(np.int64)).to(cuda),
+                                 flags=flags, filter=lf).cpu().numpy()
+    want = np.array([O.ingress_verdict(f, flags, of) for f in frames], dtype=np.uint8)
+    assert len(set(want.tolist())) >= 4
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), int(got[i]), int(want[i]), len(frames[i])) for i in bad[:10]]
