@@ -738,7 +738,9 @@ def main():
                 args.op) or {"crc32": "lnx::crc32_rows_kernel<kCrc> + lnx::crc32_stage_kernel<kCrc> (one entry; "
                                       "each slice folded by the kernel slice_kind gives it, DESIGN.md §3.10)",
                              "fcs_verify": "lnx::crc32_rows_kernel<kVerify> + lnx::crc32_stage_kernel<kVerify>",
-                       "sum16": "lnx::sum16_lines_kernel<true>", "ingress": "lnx::ingress_verify_kernel",
+                       "sum16": "lnx::sum16_lines_kernel<true>",
+                       "ingress": "lnx::ingress_verify_kernel + lnx::rx_verify_kernel<false, false> (one entry; "
+                                  "the second works when the mean frame is under 1280 B, DESIGN.md §3.12)",
                        "rx_verify": "lnx::rx_verify_kernel<true, false>",
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
