@@ -173,7 +173,10 @@ int lnx_fcs_append_batch(uint8_t* d_bytes, const uint64_t* d_start, uint32_t* d_
  * payload length only), else the frame is untouched and d_status[i] = 18
  * (lneto.ErrTruncatedFrame: too short for the IP header or for the TCP 20 /
  * UDP 8 / ICMP 8-byte header the step writes) or 15 (ErrInvalidLengthField:
- * IHL < 5, or a length over 16 bits).  Frames must not overlap. */
+ * IHL < 5, or a length over 16 bits).  Frames must not overlap.  Two
+ * launches, one of which works: the generate rows, or for a batch whose mean
+ * of 64 sampled lengths is under 896 B lnx_tx_finish_batch's checksum step
+ * (the same bytes and status; d_len is not written either way). */
 int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint32_t* d_len, uint64_t n,
                           uint8_t* d_status, void* stream);
 

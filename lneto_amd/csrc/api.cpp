@@ -49,10 +49,11 @@ hipError_t launch_crc32_segments(const uint8_t* bytes, const uint64_t* start, co
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
-                              uint8_t* status, int num_cus, hipStream_t stream);
+                              uint8_t* status, int num_cus, hipStream_t stream, uint32_t* gate = nullptr,
+                              uint32_t epoch = 0, uint64_t short_mean = 0);
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
-                            hipStream_t stream, bool host);
+                            hipStream_t stream, bool host, const uint32_t* gate = nullptr, uint32_t epoch = 0);
 hipError_t launch_sum16_segments(const uint8_t* bytes, const uint64_t* off, const uint32_t* len,
                                  const uint32_t* seed, uint64_t n, uint16_t* out, int num_cus,
                                  hipStream_t stream, int var = 0);
@@ -379,10 +380,13 @@ int get_ctx(DeviceCtx** out) {
 constexpr size_t kGiantSlots = (1u << 20) + 4096u;
 constexpr size_t kStageFlag = 2 * kGiantSlots;
 constexpr size_t kIngressGate = kStageFlag + 1;  // lnx_ingress_verify_batch's second launch (the same epoch rule)
+constexpr size_t kTxChecksumGate = kStageFlag + 2;  // lnx_tx_checksum_batch's
 constexpr size_t kScratchWords = kStageFlag + 16;
 // the mean frame length from which the ingress rows beat the receive check
 // without its CRC (tools/prof/ingress_vs_rv.py)
 constexpr uint64_t kIngressShortMean = 1280;
+// ... and the generate rows against tx_finish's checksum step (sampled mean)
+constexpr uint64_t kTxChecksumShortMean = 896;
 
 // The calling device's giant-slice scratch for `stream`, zeroed on that
 // stream when made (stream order puts the zeroing before the first launch).
@@ -598,8 +602,20 @@ int lnx_tx_checksum_batch(uint8_t* d_bytes, const uint64_t* d_start, const uint3
   DeviceCtx* c = nullptr;
   int st = get_ctx(&c);
   if (st != LNX_OK) return st;
-  hipError_t e = launch_tx_checksum(d_bytes, d_start, d_len, n, d_status, c->num_cus, static_cast<hipStream_t>(stream));
+  // two launches, one of which works (as lnx_ingress_verify_batch): the
+  // generate rows, or for a batch whose sampled mean frame is under
+  // kTxChecksumShortMean bytes tx_finish with the checksum step only
+  const hipStream_t hs = static_cast<hipStream_t>(stream);
+  uint32_t* scratch = nullptr;
+  uint32_t epoch = 0;
+  if ((st = giant_scratch(c, hs, &scratch, &epoch)) != LNX_OK) return st;
+  uint32_t* gate = scratch + kTxChecksumGate;
+  hipError_t e = launch_tx_checksum(d_bytes, d_start, d_len, n, d_status, c->num_cus, hs, gate, epoch,
+                                    kTxChecksumShortMean);
   if (e != hipSuccess) return hip_fail(e, "tx checksum (ingress_verify_kernel<GEN>) launch");
+  e = launch_tx_finish(d_bytes, d_start, const_cast<uint32_t*>(d_len), n, 0, LNX_TX_CHECKSUM, d_status, d_status,
+                       c->d_rx, c->num_cus, hs, false, gate, epoch);
+  if (e != hipSuccess) return hip_fail(e, "tx_finish_kernel launch");
   return LNX_OK;
 }
 

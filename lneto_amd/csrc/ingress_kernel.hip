@@ -114,11 +114,18 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
   // x 128 B, 2.06 against 2.61 on configs[3]'s Zipf mix; this kernel wins from
   // ~1280 B, tools/prof/ingress_vs_rv.py): every workgroup reads the batch's
   // two ends, and workgroup 0 leaves the call's epoch in the gate word
+  // lnx_tx_checksum_batch (segment mode, GEN) likewise goes to tx_finish with
+  // LNX_TX_CHECKSUM only below its crossover: tx_gate_probe (below, one wave
+  // launched first) has left the epoch in the gate word then
   if (gate) {
-    const uint64_t a = off[0], b = off[n];
-    if (b < a || b - a < short_mean * n) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) *gate = epoch;
-      return;
+    if (seg_len) {
+      if (*gate == epoch) return;
+    } else {
+      const uint64_t a = off[0], b = off[n];
+      if (b < a || b - a < short_mean * n) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *gate = epoch;
+        return;
+      }
     }
   }
   // offsets mode (seg_len null): frame f = bytes[off[f] : off[f+1] - trim];
@@ -599,18 +606,36 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
   return hipGetLastError();
 }
 
+// lnx_tx_checksum_batch's choice (0.57 against 0.75 ms on 4 M x 128 B, 2.44
+// against 2.87 on the Zipf mix for tx_finish's checksum step; the generate
+// rows win from ~900 B, tools/prof/ingress_vs_rv.py): the mean of 64 lengths
+// sampled across the batch (both kernels give the same bytes and status: the
+// sample only picks the faster).  One wave, so that the 32 K workgroups of
+// the generate rows read one word instead of 64 scattered lengths each (that
+// form cost 0.09 ms on 4 M x 1500 B: 8 M requests)
+__global__ void __launch_bounds__(64) tx_gate_probe(const uint32_t* __restrict__ len, uint64_t n, uint64_t short_mean,
+                                                    uint32_t* __restrict__ gate, uint32_t epoch) {
+  const uint64_t i = ((uint64_t)threadIdx.x * n) >> 6;
+  uint32_t l = len[i];
+#pragma unroll
+  for (int sft = 1; sft < 64; sft <<= 1) l += (uint32_t)__shfl_xor((int)l, sft);
+  if (threadIdx.x == 0 && (uint64_t)l < 64u * short_mean) *gate = epoch;  // (64 lengths < 2^25: no wrap)
+}
+
 // Batched transmit checksum generate over ring slots: frame i =
 // bytes[start[i] : start[i] + len[i]] (segment mode, trim 0), status[i] as
 // lnx_tx_checksum_batch documents.
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
-                              uint8_t* status, int num_cus, hipStream_t stream) {
+                              uint8_t* status, int num_cus, hipStream_t stream, uint32_t* gate, uint32_t epoch,
+                              uint64_t short_mean) {
   if (n == 0) return hipSuccess;
   const uint64_t frames_per_block = (kIngBlock / 64) * 4;
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   const uint64_t cap = (uint64_t)num_cus * 128;
   if (grid > cap) grid = cap;
+  if (gate) hipLaunchKernelGGL(tx_gate_probe, dim3(1), dim3(64), 0, stream, len, n, short_mean, gate, epoch);
   hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, true>), dim3((unsigned)grid), dim3(kIngBlock), 0,
-                     stream, bytes, start, n, 0u, status, len, 0u, RxFilter{}, nullptr, 0u, 0ull);
+                     stream, bytes, start, n, 0u, status, len, 0u, RxFilter{}, gate, epoch, short_mean);
   return hipGetLastError();
 }
 

@@ -71,12 +71,13 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
                                  uint32_t trim, const RxFilter* filter, uint32_t* gate = nullptr, uint32_t epoch = 0,
                                  uint64_t short_mean = 0);
 hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint32_t* len, uint64_t n,
-                              uint8_t* status, int num_cus, hipStream_t stream);
+                              uint8_t* status, int num_cus, hipStream_t stream, uint32_t* gate = nullptr,
+                              uint32_t epoch = 0, uint64_t short_mean = 0);
 hipError_t launch_fcs_append(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                              uint8_t* status, const void* images, int num_cus, hipStream_t stream, int var = 0);
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
-                            hipStream_t stream, bool host);
+                            hipStream_t stream, bool host, const uint32_t* gate = nullptr, uint32_t epoch = 0);
 
 // Slot i of the batch: frame = slot[offset : min(len, cap)].
 __global__ void __launch_bounds__(256)

@@ -833,7 +833,10 @@ template <bool FCS, bool CK, bool HOST>
 __global__ void __launch_bounds__(HOST ? kTxBlockHost : kTxBlock)
 tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start, uint32_t* __restrict__ len,
                  uint32_t n, uint32_t capacity, uint8_t* __restrict__ st_ck, uint8_t* __restrict__ st_ap,
-                 const uint32_t* __restrict__ image, uint32_t gsz) {
+                 const uint32_t* __restrict__ image, uint32_t gsz, const uint32_t* __restrict__ gate, uint32_t epoch) {
+  // behind the generate rows (lnx_tx_checksum_batch on a short-frame batch,
+  // launch_tx_checksum): nothing to do unless they left this call's epoch
+  if (gate && *gate != epoch) return;
   constexpr uint32_t kB = HOST ? kTxBlockHost : kTxBlock;
   constexpr uint32_t kTabBytes = FCS ? kTxTabBytes : 0u;
   constexpr uint32_t kWaveBytes = kTxGroup * 8u * (1u + kRvHead);
@@ -1071,7 +1074,8 @@ tx_finish_kernel(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ start
           }
         }
       }
-      len[fk] = app ? Lp + 4u : L;
+      if constexpr (FCS) len[fk] = app ? Lp + 4u : L;  // (the checksum step alone leaves the lengths: const for
+                                                       // lnx_tx_checksum_batch, which may run this kernel)
       const uint32_t ap = FCS && !app ? 6u : 0u;
       if (st_ap == st_ck) {  // one status array: the checksum step's if non-zero, else the append's
         st_ck[fk] = (uint8_t)(v ? v : ap);
@@ -1123,7 +1127,7 @@ uint32_t balanced_group(uint64_t n, uint64_t waves, uint32_t gmax) {
 
 hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len, uint64_t n, uint32_t capacity,
                             uint32_t flags, uint8_t* st_ck, uint8_t* st_ap, const uint32_t* image, int num_cus,
-                            hipStream_t stream, bool host) {
+                            hipStream_t stream, bool host, const uint32_t* gate, uint32_t epoch) {
   const bool ck = flags & 1u, fcs = flags & 2u;
   // batches of up to 2^31 frames (the kernel's 32-bit frame indices)
   for (uint64_t f0 = 0; f0 < n; f0 += 1ull << 31) {
@@ -1135,7 +1139,7 @@ hipError_t launch_tx_finish(uint8_t* bytes, const uint64_t* start, uint32_t* len
     uint8_t* sa = st_ap == st_ck ? st_ck + f0 : st_ap + f0;
 #define LNX_TX(A, C, H)                                                                                                 \
   hipLaunchKernelGGL((tx_finish_kernel<A, C, H>), dim3((unsigned)grid), dim3((unsigned)blk), 0, stream, bytes, start + f0, \
-                     len + f0, m, capacity, st_ck + f0, sa, image, gsz)
+                     len + f0, m, capacity, st_ck + f0, sa, image, gsz, gate, epoch)
     if (host) {
       if (fcs) {
         if (ck) LNX_TX(true, true, true); else LNX_TX(true, false, true);

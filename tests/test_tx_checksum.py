@@ -212,3 +212,51 @@ def test_gpu_tx_checksum_then_ingress_verify(cuda):
     want = [O.ingress_verdict(img[s:e].tobytes(), O.VERIFY_ICMP) for s, e in zip(starts, ends)]
     assert vi.tolist() == want
     assert O.ERR_BAD_CRC not in want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("route", ["tx_finish", "generate_rows"])
+@pytest.mark.parametrize("base_pad", [0, 3])
+def test_gpu_tx_checksum_both_routes(cuda, route, base_pad):
+    """lnx_tx_checksum_batch launches the generate rows and tx_finish's checksum
+    step, and the one the batch's sampled mean length picks works (api.cpp
+    kTxChecksumShortMean, 896 B over 64 lengths spread across the batch): the
+    generator's frames under 600 B alone (tx_finish), and after as many jumbo
+    frames (the generate rows); bytes and status against the oracle, the bytes
+    between the frames and the length array untouched either way."""
+    import torch
+    import lneto_amd as L
+    rng = np.random.default_rng(70 + base_pad)
+    short = [f for f in tx_frames(seed=60 + base_pad, count=3000) if len(f) < 600]
+    frames = list(short)
+    if route == "generate_rows":
+        jumbo = []
+        for _ in range(len(short)):
+            b = bytearray(G.ether(0x0800, G.ipv4(int(rng.choice([6, 17])), G.tcp(
+                rng.integers(0, 256, int(rng.integers(3000, 8900)), dtype=np.uint8).tobytes()), fix_l4=False)))
+            b[24:26] = rng.integers(0, 256, 2, dtype=np.uint8).tobytes()  # stale header CRC
+            jumbo.append(bytes(b))
+        frames = jumbo + short
+    n = len(frames)
+    idx = [(i * n) >> 6 for i in range(64)]
+    assert (sum(len(frames[i]) for i in idx) < 64 * 896) == (route == "tx_finish")
+    buf, starts, lens = _pack_slots(frames, 9100, base_pad)
+    d = torch.from_numpy(buf).to(cuda)
+    d_len = torch.from_numpy(lens).to(cuda)
+    st = L.tx_checksum_batch(d, torch.from_numpy(starts).to(cuda), d_len).cpu().numpy()
+    host = d.cpu().numpy()
+    assert np.array_equal(d_len.cpu().numpy(), lens)
+    bad = []
+    codes = set()
+    for i, f in enumerate(frames):
+        want, ws = O.tx_checksum(f)
+        codes.add(ws)
+        s = int(starts[i])
+        if host[s:s + len(f)].tobytes() != want or int(st[i]) != ws:
+            bad.append((i, len(f), int(st[i]), ws))
+    assert not bad, bad[:10]
+    assert len(codes) >= 3
+    mask = np.ones(len(buf), dtype=bool)
+    for i, f in enumerate(frames):
+        mask[starts[i]:starts[i] + len(f)] = False
+    assert np.array_equal(host[mask], buf[mask])
