@@ -344,11 +344,25 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
       const int32_t lastq = QE - 1, qL = (int32_t)((L + mis) >> 3);
       const int32_t qme = (lastq & 15) == (int32_t)p ? lastq : (qL & 15) == (int32_t)p && qL < lastq ? qL : -1;
       uint2 ye = make_uint2(0u, 0u);
+      // short passes (every row's window within 4 lines, the Zipf mix): the
+      // qword(s) at the end are taken as the fold passes them, 8 selects,
+      // rather than loaded again after it (an L2 round trip at the end of the
+      // pass); MTU passes (12 lines: 24 selects) load it again.  Receive only:
+      // in the transmit kernel it bought 0.9 % on Zipf and cost 0.4 % on MTU
+      // frames (A/B x4, r8a); receive: Zipf -1.4 %, ingress's Zipf -2.7 %
+      const bool cap4 = !HOST && !TX && nlw <= 4;
       auto capture = [&](const uint2 (&y)[kRvUnroll], int it) {
         if constexpr (HOST) {
 #pragma unroll
           for (int u = 0; u < kRvUnroll; ++u) {
             const bool at = (int32_t)p + 16 * (u + kRvUnroll * it) == qme;
+            ye.x = at ? y[u].x : ye.x;
+            ye.y = at ? y[u].y : ye.y;
+          }
+        } else if (it == 0 && cap4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const bool at = (int32_t)p + 16 * u == qme;
             ye.x = at ? y[u].x : ye.x;
             ye.y = at ? y[u].y : ye.y;
           }
@@ -426,7 +440,9 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
 #pragma unroll
         for (int u = 0; u < kRvUnroll; ++u) fold(y[u], u, it, u + kRvUnroll * it < NL);
       }
-      if constexpr (!HOST) ye = rv_ld(qme >= 0 ? base2 + qme : zero);  // (an L2 hit: the fold just read it)
+      if constexpr (!HOST) {
+        if (!cap4) ye = rv_ld(qme >= 0 ? base2 + qme : zero);  // (an L2 hit: the fold just read it)
+      }
       const int32_t oe = 8 * qme - (int32_t)mis;
       S -= rv_dot2(ye.x & rv_keep_from((int32_t)L - oe), rv_dot2(ye.y & rv_keep_from((int32_t)L - oe - 4), 0u)) &
            (qme >= 0 && L >= 14 ? ~0u : 0u);
