@@ -211,6 +211,174 @@ constexpr int kTxPf = LNX_TX_PF;   // ... (the transmit kernel over device memor
 constexpr int kRvPfRx = LNX_RV_PF_RX;  // ... (receive: the whole next pass)
 __device__ uint2 g_rv_zero[2];
 
+typedef uint32_t rv_u4 __attribute__((ext_vector_type(4)));
+__device__ __attribute__((aligned(16))) uint32_t g_rv_zero4[4];
+__device__ __forceinline__ rv_u4 rv_ld4(const rv_u4* p) {
+  return *(const __attribute__((address_space(1))) rv_u4*)p;
+}
+// the XOR / sum over an 8-lane row (two quad steps, then the other quad of the half row)
+__device__ __forceinline__ uint32_t rv_row8_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return v;
+}
+__device__ __forceinline__ uint32_t rv_row8_add(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+  return v;
+}
+
+// Phase A for the group's short frames (round 6): positions [0, n8) of the
+// passes' order, every frame there at most 384 bytes (length class <= 3, so
+// its window is at most 4 lines), in passes of EIGHT 8-lane rows.  Lane p of a
+// row loads the 16-byte blocks p, p + 8, p + 16, p + 24 of a window that
+// starts at the 16-byte block holding the frame's first byte (one dwordx4 a
+// line: a row still reads a whole 128-byte line per instruction, and a block
+// that holds a frame byte never leaves its page), i.e. qwords 2p and 2p + 1 of
+// each line: lane p plays the lanes 2p and 2p + 1 of the 16-lane rows, with a
+// CRC register each, the same fold, masks and end corrections (the window's
+// misalignment m16 < 16 in place of mis < 8), the two registers shifted by
+// F_{2p+a} and F_{2p+1+a} and XORed over the row.  The per-pass work of a row
+// (the frame's start and length, its masks, the shifts) then serves eight
+// frames a wave instead of four.
+template <bool CRC, bool TX>
+__device__ __forceinline__ void rv_rows8(const char* lds, uint2* res, uint2* head, const RvLane& z,
+                                         const uint8_t* bytes, uint64_t sk, uint32_t Ltk, uint32_t n8, uint32_t trim,
+                                         uint32_t capacity) {
+  // (the lane index opaque here: values derived from it are computed where
+  // they are used, not hoisted to the kernel's entry and held, or spilled,
+  // through the 16-lane passes; this function is the receive kernel's
+  // register peak)
+  uint32_t lane = threadIdx.x & 63u;
+  asm volatile("" : "+v"(lane));
+  const uint32_t p = lane & 7u, row = lane >> 3;
+  const rv_u4* zero4 = reinterpret_cast<const rv_u4*>(g_rv_zero4);
+  auto wave_max = [&](int32_t x) -> int32_t {
+    x = max(x, __shfl_xor(x, 8));
+    x = max(x, __shfl_xor(x, 16));
+    x = max(x, __shfl_xor(x, 32));
+    return __builtin_amdgcn_readfirstlane(x);
+  };
+  auto row_frame = [&](uint32_t j, const uint8_t*& fr, uint32_t& Lt) {
+    const uint32_t k = 8u * j + row;
+    const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
+    const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
+    Lt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ltk);
+    fr = bytes + (((uint64_t)shi << 32) | slo);
+  };
+  // a pass's four lines: the blocks some byte of the row's frame lies in (the
+  // rest zero, without a load), the second qword of a block past the frame's
+  // last qword zeroed (the 16-lane rows never load it)
+  // (the next pass's first two lines are loaded a pass ahead, the other two
+  // in the pass: four ahead spilled the receive kernel's registers)
+  constexpr int PQ = 2;
+  rv_u4 pf[PQ];
+  const uint8_t* frn = bytes;
+  uint32_t Ltn = 0;
+  auto blocks = [&](const uint8_t* f, uint32_t Lt, const rv_u4*& b4, int32_t& QB, int32_t& um) {
+    const uint32_t m16 = (uint32_t)(reinterpret_cast<uintptr_t>(f) & 15u);
+    b4 = reinterpret_cast<const rv_u4*>(f - m16);
+    QB = (int32_t)((Lt + m16 + 15u) >> 4);
+    um = (wave_max(QB) + 7) >> 3;
+  };
+  auto prefetch = [&](uint32_t jn) {
+    if (8u * jn >= n8) return;  // (wave-uniform)
+    row_frame(jn, frn, Ltn);
+    const rv_u4* b4;
+    int32_t QB, um;
+    blocks(frn, Ltn, b4, QB, um);
+#pragma unroll
+    for (int u = 0; u < PQ; ++u) {
+      const int32_t b = (int32_t)p + 8 * u;
+      pf[u] = u < um ? rv_ld4(b < QB ? b4 + b : zero4) : rv_u4{0u, 0u, 0u, 0u};
+    }
+  };
+  prefetch(0);
+  for (uint32_t j = 0; 8u * j < n8; ++j) {
+    // (the row index made opaque in every pass: hoisted out of the loops, the
+    // head and result addresses derived from it were spilled)
+    uint32_t rw = row;
+    asm volatile("" : "+v"(rw));
+    const uint32_t k = 8u * j + rw;
+    const uint8_t* fr = frn;
+    const uint32_t Lt = Ltn;
+    rv_u4 y[4];
+#pragma unroll
+    for (int u = 0; u < PQ; ++u) y[u] = pf[u];
+    {
+      const rv_u4* b4;
+      int32_t QB, um;
+      blocks(fr, Lt, b4, QB, um);
+#pragma unroll
+      for (int u = PQ; u < 4; ++u) {
+        const int32_t b = (int32_t)p + 8 * u;
+        y[u] = u < um ? rv_ld4(b < QB ? b4 + b : zero4) : rv_u4{0u, 0u, 0u, 0u};
+      }
+    }
+    prefetch(j + 1u);
+    const uint32_t Lc = TX && CRC && (Lt < 60u ? 60u : Lt) + 4u <= capacity ? (Lt < 60u ? 60u : Lt) : Lt;
+    const uint32_t L = TX ? Lt : (Lt > trim ? Lt - trim : 0u);
+    const uint32_t m16 = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 15u);
+    const int32_t QE = (int32_t)((Lt + m16 + 7u) >> 3);  // qwords holding frame bytes (from the 16-byte block)
+    const int32_t NL = (int32_t)(((Lc + m16 + 7u) >> 3) + 15u) >> 4;  // lines of the CRC window (<= 4)
+    const int32_t nlw = wave_max(NL);
+    uint32_t S = 0, r[2] = {0u, 0u};
+    // the frame's first qwords for phase B (from the 8-byte-aligned base it uses)
+    const int32_t hsh = m16 >= 8u ? 1 : 0;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int32_t q2 = 2 * (int32_t)p + v - hsh;
+      if (q2 >= 0 && q2 < (int32_t)kRvHead)  // (qwords past the frame as zero, as the 16-lane rows stage them)
+        head[kRvHead * k + q2] = 2 * (int32_t)p + v >= QE ? make_uint2(0u, 0u)
+                                 : v ? make_uint2(y[0][2], y[0][3]) : make_uint2(y[0][0], y[0][1]);
+    }
+    // every qword masked as it is folded (the sum to [14, L), the CRC to
+    // [0, Lt) with the init on [0, 4)), so no end correction follows: the
+    // 16-lane rows' reload of the end qwords and their junk unit kept more
+    // registers live than the kernel has
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u > 0 && u >= nlw) break;  // (wave-uniform: no row's window reaches line u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int32_t o = 8 * (2 * (int32_t)p + v + 16 * u) - (int32_t)m16;  // the qword's first frame offset
+        const uint32_t c0 = y[u][2 * v], c1 = y[u][2 * v + 1];
+        if (u == 0) {
+          S = rv_dot2(c0 & rv_range(o, 14, (int32_t)L), rv_dot2(c1 & rv_range(o + 4, 14, (int32_t)L), S));
+        } else {
+          S = rv_dot2(c0 & ~rv_keep_from((int32_t)L - o), rv_dot2(c1 & ~rv_keep_from((int32_t)L - o - 4), S));
+        }
+        if constexpr (CRC) {
+          const int32_t ie = (int32_t)(Lc < 4 ? Lc : 4u);
+          uint32_t d0, d1;
+          if (u == 0) {
+            d0 = (c0 & rv_range(o, 0, (int32_t)Lt)) ^ rv_range(o, 0, ie);
+            d1 = (c1 & rv_range(o + 4, 0, (int32_t)Lt)) ^ rv_range(o + 4, 0, ie);
+          } else {
+            d0 = c0 & ~rv_keep_from((int32_t)Lt - o);
+            d1 = c1 & ~rv_keep_from((int32_t)Lt - o - 4);
+          }
+          const uint32_t nr = rv_unit(lds, r[v] ^ d0, d1, z);
+          r[v] = u < NL ? nr : r[v];
+        }
+      }
+    }
+    uint32_t okf = 1;
+    if constexpr (CRC) {
+      // the window ends W = 128 NL - m16 past the frame start; W - Lc = 8a + b
+      const uint32_t pad = (uint32_t)(128 * NL - (int32_t)m16 - (int32_t)Lc);
+      const uint32_t a = pad >> 3, b = pad & 7u;
+      const uint32_t x = rv_row8_xor(rv_nib_f(lds, 2u * p + a, r[0]) ^ rv_nib_f(lds, 2u * p + 1u + a, r[1]));
+      const uint32_t R = rv_nib(lds, kRvB + 512u * b, x);
+      okf = TX ? R : (uint32_t)(Lt >= 4 && ~R == 0x2144DF1Cu);
+    }
+    S = rv_row8_add(S);
+    if (p == 0) res[k] = make_uint2(okf, S);
+  }
+}
+
 // Phase A of a group (see above): kRvGroup / 4 passes of four 16-lane rows.
 // Lane k < kRvGroup holds its frame's start sk and length Ltk.  Per frame the
 // rows load the bytes [0, Ld), fold the CRC over them followed by zeros up to
@@ -240,8 +408,10 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
     // memory: over PCIe the passes keep address order (the ring's zero-copy
     // receive on the Zipf mix ran 7.10 -> 7.44 ms per 1 M frames sorted).
     uint32_t rank = lane;
+    uint32_t n8 = 0;  // positions [0, n8): the 8-lane rows (rv_rows8)
     if constexpr (!HOST) {
       const uint32_t key = lane < nrow ? ((Ltk + 127u) >> 7 < 14u ? (Ltk + 127u) >> 7 : 14u) : 15u;
+      n8 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(key <= 3u)) & ~7u;
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
       if (__builtin_amdgcn_ballot_w64(lane < nrow && key != k0) != 0) {
         uint32_t below = 0;
@@ -252,16 +422,21 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
           below += key > c ? (uint32_t)__builtin_popcountll(m) : 0u;
           same = key == c ? m : same;
         }
-        rank = below + (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
+        // (the lanes of `same` below this one by mbcnt: no lane mask held in registers)
+        rank = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
         const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)(uint32_t)sk);
         const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)(uint32_t)(sk >> 32));
         Ltk = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank << 2), (int)Ltk);
         sk = ((uint64_t)shi << 32) | slo;
       }
     }
+    // the short frames (length class <= 3, sorted first) in 8-lane rows, the rest below
+    if constexpr (!HOST) {
+      if (n8 > 0) rv_rows8<CRC, TX>(lds, res, head, z, bytes, sk, Ltk, n8, trim, capacity);
+    }
     // the row's frame of pass j: its start (from the lane that holds it) and length
     auto row_frame = [&](uint32_t j, const uint8_t*& fr, uint32_t& Lt) {
-      const uint32_t k = 4u * j + row;
+      const uint32_t k = n8 + 4u * j + row;
       const uint32_t slo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)sk);
       const uint32_t shi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)(uint32_t)(sk >> 32));
       Lt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(k << 2), (int)Ltk);
@@ -288,7 +463,7 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
       return __builtin_amdgcn_readfirstlane(x);
     };
     auto prefetch = [&](int slot, uint32_t jn) {
-      if (4u * jn >= nrow) return;  // (wave-uniform)
+      if (n8 + 4u * jn >= nrow) return;  // (wave-uniform)
       row_frame(jn, frn[slot], Ltn[slot]);
       const uint32_t m2 = (uint32_t)(reinterpret_cast<uintptr_t>(frn[slot]) & 7u);
       const uint2* b2 = reinterpret_cast<const uint2*>(frn[slot] - m2);
@@ -317,8 +492,8 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
     };
 #pragma unroll
     for (int a = 0; a < PR; ++a) prefetch(a, (uint32_t)a);
-    for (uint32_t j = 0; 4u * j < nrow; ++j) {
-      const uint32_t k = 4u * j + row;  // the row's frame in the group (its sorted position)
+    for (uint32_t j = 0; n8 + 4u * j < nrow; ++j) {
+      const uint32_t k = n8 + 4u * j + row;  // the row's frame in the group (its sorted position)
       const uint8_t* fr = frn[0];
       // Lt: the bytes loaded and folded; Lc: the CRC's length (zeros past Lt); L: the sum's end
       const uint32_t Lt = Ltn[0];
@@ -506,13 +681,16 @@ rx_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
   for (uint64_t g = (uint64_t)blockIdx.x * (kRvBlock / 64) + wv; g < ngroups; g += (uint64_t)gridDim.x * (kRvBlock / 64)) {
     // the group's frames: lane k < gsz holds frame g * gsz + k's start and length (FCS included)
     const uint64_t fk = g * gsz + lane;
-    const bool live = lane < gsz && fk < n;
+    // (32-bit compares on the scalar unit: the 64-bit one, which SALU lacks,
+    // held gsz in a VGPR pair through the whole kernel)
+    const uint64_t rem = n - g * gsz;
+    const uint32_t nrow = (uint32_t)(rem >> 32) != 0u || (uint32_t)rem >= gsz ? gsz : (uint32_t)rem;
+    const bool live = lane < nrow;
     const uint64_t fi = live ? fk : n - 1u;
     const uint64_t sk = off[fi];
     const uint64_t ek = seg_len ? sk + seg_len[fi] : off[fi + 1];
     const uint64_t ltk = live && ek > sk ? ek - sk : 0u;
     const uint32_t Ltk = ltk < 0x7FFFFFFFull ? (uint32_t)ltk : 0x7FFFFFFFu;
-    const uint32_t nrow = (uint32_t)(n - g * gsz < gsz ? n - g * gsz : gsz);
 
     // ---------------------------------------------------------------- A: data
     // (the whole next pass loaded ahead from HBM: 0.335 against 0.340-0.344 ms for 8 of
