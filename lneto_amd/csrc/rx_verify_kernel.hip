@@ -212,6 +212,15 @@ constexpr int kRvPfRx = LNX_RV_PF_RX;  // ... (receive: the whole next pass)
 __device__ uint2 g_rv_zero[2];
 
 typedef uint32_t rv_u4 __attribute__((ext_vector_type(4)));
+#ifndef LNX_RV_R8_LINES
+#define LNX_RV_R8_LINES 10
+#endif
+// lines of the 8-lane rows' window: frames of length class < kR8Lines (at
+// most 128 (kR8Lines - 1) bytes, so a window of <= kR8Lines lines) take them.
+// 10 (frames to 1152 B): against 4, 0.59 against 0.67 ms on 4 M x 768 B,
+// 0.76 against 0.79 at 1024 B, the Zipf mix 1-3 % faster; 13 (MTU frames
+// too) made the 1 M x 1500 B receive check 13 % slower (profiles/r8f)
+constexpr int kR8Lines = LNX_RV_R8_LINES;
 __device__ __attribute__((aligned(16))) uint32_t g_rv_zero4[4];
 __device__ __forceinline__ rv_u4 rv_ld4(const rv_u4* p) {
   return *(const __attribute__((address_space(1))) rv_u4*)p;
@@ -231,8 +240,8 @@ __device__ __forceinline__ uint32_t rv_row8_add(uint32_t v) {
 }
 
 // Phase A for the group's short frames (round 6): positions [0, n8) of the
-// passes' order, every frame there at most 384 bytes (length class <= 3, so
-// its window is at most 4 lines), in passes of EIGHT 8-lane rows.  Lane p of a
+// passes' order, every frame there at most 128 (kR8Lines - 1) bytes (its
+// window at most kR8Lines lines), in passes of EIGHT 8-lane rows.  Lane p of a
 // row loads the 16-byte blocks p, p + 8, p + 16, p + 24 of a window that
 // starts at the 16-byte block holding the frame's first byte (one dwordx4 a
 // line: a row still reads a whole 128-byte line per instruction, and a block
@@ -304,7 +313,7 @@ __device__ __forceinline__ void rv_rows8(const char* lds, uint2* res, uint2* hea
     const uint32_t k = 8u * j + rw;
     const uint8_t* fr = frn;
     const uint32_t Lt = Ltn;
-    rv_u4 y[4];
+    rv_u4 y[kR8Lines];
 #pragma unroll
     for (int u = 0; u < PQ; ++u) y[u] = pf[u];
     {
@@ -312,7 +321,7 @@ __device__ __forceinline__ void rv_rows8(const char* lds, uint2* res, uint2* hea
       int32_t QB, um;
       blocks(fr, Lt, b4, QB, um);
 #pragma unroll
-      for (int u = PQ; u < 4; ++u) {
+      for (int u = PQ; u < kR8Lines; ++u) {
         const int32_t b = (int32_t)p + 8 * u;
         y[u] = u < um ? rv_ld4(b < QB ? b4 + b : zero4) : rv_u4{0u, 0u, 0u, 0u};
       }
@@ -322,7 +331,7 @@ __device__ __forceinline__ void rv_rows8(const char* lds, uint2* res, uint2* hea
     const uint32_t L = TX ? Lt : (Lt > trim ? Lt - trim : 0u);
     const uint32_t m16 = (uint32_t)(reinterpret_cast<uintptr_t>(fr) & 15u);
     const int32_t QE = (int32_t)((Lt + m16 + 7u) >> 3);  // qwords holding frame bytes (from the 16-byte block)
-    const int32_t NL = (int32_t)(((Lc + m16 + 7u) >> 3) + 15u) >> 4;  // lines of the CRC window (<= 4)
+    const int32_t NL = (int32_t)(((Lc + m16 + 7u) >> 3) + 15u) >> 4;  // lines of the CRC window (<= kR8Lines)
     const int32_t nlw = wave_max(NL);
     uint32_t S = 0, r[2] = {0u, 0u};
     // the frame's first qwords for phase B (from the 8-byte-aligned base it uses)
@@ -339,7 +348,7 @@ __device__ __forceinline__ void rv_rows8(const char* lds, uint2* res, uint2* hea
     // 16-lane rows' reload of the end qwords and their junk unit kept more
     // registers live than the kernel has
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kR8Lines; ++u) {
       if (u > 0 && u >= nlw) break;  // (wave-uniform: no row's window reaches line u)
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
@@ -411,7 +420,7 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
     uint32_t n8 = 0;  // positions [0, n8): the 8-lane rows (rv_rows8)
     if constexpr (!HOST) {
       const uint32_t key = lane < nrow ? ((Ltk + 127u) >> 7 < 14u ? (Ltk + 127u) >> 7 : 14u) : 15u;
-      n8 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(key <= 3u)) & ~7u;
+      n8 = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(key < (uint32_t)kR8Lines)) & ~7u;
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
       if (__builtin_amdgcn_ballot_w64(lane < nrow && key != k0) != 0) {
         uint32_t below = 0;
@@ -430,7 +439,7 @@ __device__ __forceinline__ uint32_t rv_rows(const char* lds, uint2* res, uint2* 
         sk = ((uint64_t)shi << 32) | slo;
       }
     }
-    // the short frames (length class <= 3, sorted first) in 8-lane rows, the rest below
+    // the short frames (length class < kR8Lines, sorted first) in 8-lane rows, the rest below
     if constexpr (!HOST) {
       if (n8 > 0) rv_rows8<CRC, TX>(lds, res, head, z, bytes, sk, Ltk, n8, trim, capacity);
     }
