@@ -115,7 +115,7 @@ ingress_verify_kernel(IngBytes<GEN>* __restrict__ bytes, const uint64_t* __restr
   // ~1280 B, tools/prof/ingress_vs_rv.py): every workgroup reads the batch's
   // two ends, and workgroup 0 leaves the call's epoch in the gate word
   // lnx_tx_checksum_batch (segment mode, GEN) likewise goes to tx_finish with
-  // LNX_TX_CHECKSUM only below its crossover: tx_gate_probe (below, one wave
+  // LNX_TX_CHECKSUM only below its crossover: tx_gate_probe_kernel (below, one wave
   // launched first) has left the epoch in the gate word then
   if (gate) {
     if (seg_len) {
@@ -613,7 +613,7 @@ hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint
 // sample only picks the faster).  One wave, so that the 32 K workgroups of
 // the generate rows read one word instead of 64 scattered lengths each (that
 // form cost 0.09 ms on 4 M x 1500 B: 8 M requests)
-__global__ void __launch_bounds__(64) tx_gate_probe(const uint32_t* __restrict__ len, uint64_t n, uint64_t short_mean,
+__global__ void __launch_bounds__(64) tx_gate_probe_kernel(const uint32_t* __restrict__ len, uint64_t n, uint64_t short_mean,
                                                     uint32_t* __restrict__ gate, uint32_t epoch) {
   const uint64_t i = ((uint64_t)threadIdx.x * n) >> 6;
   uint32_t l = len[i];
@@ -633,7 +633,7 @@ hipError_t launch_tx_checksum(uint8_t* bytes, const uint64_t* start, const uint3
   uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
   const uint64_t cap = (uint64_t)num_cus * 128;
   if (grid > cap) grid = cap;
-  if (gate) hipLaunchKernelGGL(tx_gate_probe, dim3(1), dim3(64), 0, stream, len, n, short_mean, gate, epoch);
+  if (gate) hipLaunchKernelGGL(tx_gate_probe_kernel, dim3(1), dim3(64), 0, stream, len, n, short_mean, gate, epoch);
   hipLaunchKernelGGL((ingress_verify_kernel<kIngUnrollQ, true, true>), dim3((unsigned)grid), dim3(kIngBlock), 0,
                      stream, bytes, start, n, 0u, status, len, 0u, RxFilter{}, gate, epoch, short_mean);
   return hipGetLastError();

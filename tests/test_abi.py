@@ -125,8 +125,8 @@ def test_product_library_holds_only_product_kernels():
     # ingress: filtered / unfiltered verdicts, TX generate; rx_verify: (FCS / none) x (filter / none) x
     # (HBM / host memory); tx_finish: (FCS / none) x (checksum / none) x (HBM / host memory)
     assert others == (["crc32_search_o_kernel"] + ["crc32_stage_kernel"] * 2 + ["ingress_verify_kernel"] * 3 +
-                      ["ring_segments_kernel"] + ["rx_verify_kernel"] * 8 + ["sum16_lines_kernel"] +
-                      ["tx_finish_kernel"] * 8), others
+                      ["ring_segments_kernel"] + ["rx_verify_kernel"] * 8 + ["sum16_lines_kernel"] + ["tx_finish_kernel"] * 8 +
+                      ["tx_gate_probe_kernel"]), others
     stage = [k for k in ks if "crc32_stage_kernel" in k]
     assert all(re.search(r"crc32_stage_kernelILNS_9StageModeE\dEEEv", k) for k in stage), stage  # CRC / verify only
     research = os.path.join(os.path.dirname(L.LIB_PATH), "liblneto_amd_research.so")
