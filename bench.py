@@ -426,7 +426,7 @@ def main():
                     choices=["auto", "mtu1500", "mtu1500_x8", "jumbo9000", "zipf64_1500"])
     ap.add_argument("--op", default="crc32",
                     choices=["crc32", "fcs_verify", "fcs_append", "tx_finish", "sum16", "ingress", "rx_ring", "search",
-                             "tx_checksum", "egress_packets", "ingress_packets", "rx_verify"])
+                             "tx_checksum", "egress_packets", "ingress_packets", "rx_verify", "pcap"])
     ap.add_argument("--short-frames", action="store_true",
                     help="--op crc32 / fcs_verify through lnx_*_batch_ex(LNX_BATCH_SHORT_FRAMES): the staged "
                          "lane-stream kernel the caller picks for a short-frame mix (DESIGN.md §3.9)")
@@ -575,7 +575,7 @@ def main():
         fcs = L.crc32_segments(d_bytes, starts, lens)
         fr[:, flen - 4:] = fcs.view(torch.uint8).view(n_local, 4)
         d_hit = torch.empty(n_local, dtype=torch.int64, device=dev)
-    elif args.op in ("ingress", "tx_checksum", "rx_verify") and flen is None:
+    elif args.op in ("ingress", "tx_checksum", "rx_verify", "pcap") and flen is None:
         # the Zipf mix (64-1500 B on the wire) packed back to back: every frame a
         # valid UDP/IPv4 packet (rx_verify: with its LE FCS), so each takes the
         # full header-sum + UDP-sum path and is accepted
@@ -586,7 +586,7 @@ def main():
         if args.op == "tx_checksum":
             d_seg = d_off[:-1].contiguous()
             d_len = d_lens.to(torch.int32)
-    elif args.op in ("ingress", "tx_checksum", "rx_verify"):
+    elif args.op in ("ingress", "tx_checksum", "rx_verify", "pcap"):
         if flen < 42:
             raise SystemExit(f"--op {args.op} needs frames of at least 42 bytes")
         fr = d_bytes[: n_local * flen].view(n_local, flen)
@@ -618,6 +618,8 @@ def main():
             L.ingress_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "rx_verify":
             L.rx_verify_batch(d_bytes, d_off, out=(d_ok, d_verdict), stream=stream)
+        elif args.op == "pcap":
+            L.pcap_verify_batch(d_bytes, d_off, out=d_ok, stream=stream)
         elif args.op == "tx_checksum":
             L.tx_checksum_batch(d_bytes, d_seg, d_len, status=d_ok, stream=stream)
         elif args.op == "search":
@@ -700,6 +702,7 @@ def main():
         "fcs_append": "GiB/s TX FCS append (pad, CRC-32, LE32 store) over device-resident ring slots",
         "tx_finish": "GiB/s transmit tail in one read (checksum generate + pad + FCS) over device-resident ring slots",
         "tx_checksum": "GiB/s TX checksum generate (IPv4 header + UDP) over device-resident frames",
+        "pcap": "GiB/s pcap checksum re-verification (IPv4 header + UDP, capture.go semantics) over device-resident frames",
     }[args.op]
     out = {
         "metric": metric,
@@ -745,7 +748,8 @@ def main():
                        "search": "lnx::crc32_search_o_kernel",
                        "fcs_append": "lnx::crc32_rows_kernel<kAppend> (segment mode, one launch)",
                        "tx_finish": "lnx::tx_finish_kernel<FCS, CK, HBM>",
-                       "tx_checksum": "lnx::ingress_verify_kernel<GEN>"}[args.op],
+                       "tx_checksum": "lnx::ingress_verify_kernel<GEN>",
+                       "pcap": "lnx::pcap_verify_kernel"}[args.op],
             "kernel_ms": round(kern_ms, 4),
             "kernel_ms_window": f"HIP events around all {args.steps} timed steps on the launch stream, / {args.steps}",
             "algorithmic_bytes_per_launch": nbytes,
@@ -805,7 +809,7 @@ def main():
         if args.op == "sum16":
             got = d_sum.cpu().numpy().view(np.uint16)
             seeds = d_seed.cpu().numpy().view(np.uint32)
-        elif args.op in ("fcs_verify", "ingress", "tx_checksum"):
+        elif args.op in ("fcs_verify", "ingress", "tx_checksum", "pcap"):
             got = d_ok.cpu().numpy()
         elif args.op == "rx_verify":
             got = d_ok.cpu().numpy().astype(np.uint32) * 256 + d_verdict.cpu().numpy()
@@ -835,6 +839,8 @@ def main():
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C)
             elif args.op == "ingress":
                 want = O.ingress_verdict(fr)
+            elif args.op == "pcap":
+                want = O.pcap_checksums(fr)
             elif args.op == "rx_verify":
                 want = int(len(fr) >= 4 and O.crc32(fr) == 0x2144DF1C) * 256 + O.ingress_verdict(fr[:-4] if len(fr) >= 4 else b"")
             elif args.op == "tx_checksum":

@@ -90,6 +90,24 @@ uint16_t lnx_never_zero_sum(uint16_t sum16);
 struct lnx_rx_filter;
 int lnx_ingress_verdict(const uint8_t* frame, size_t len, uint32_t flags, const struct lnx_rx_filter* filter);
 
+/* pcap's checksum re-verification of ONE Ethernet frame on the host: what
+ * PacketBreakdown.CaptureEthernet records about the frame's checksums
+ * (internet/pcap/capture.go:67-277), which differs from the receive path's
+ * verdict: a bad IPv4 header sum is recorded and the transport check still
+ * runs (:229-231); on IPv4 the TCP / UDP checks run only when tcp / udp.NewFrame
+ * accept the payload (:241-266), a UDP checksum of 0 is not checked (:259),
+ * ICMPv4 is always summed with no pseudo-header (:267-273); IPv6 sums UDP and
+ * UDPLite over the UDP length (:184-198).  Returns the status byte (>= 0):
+ * LNX_PCAP_IP_HDR_BAD | LNX_PCAP_PROTO_BAD | code << 2, code = the errGeneric
+ * value (15 ErrInvalidLengthField, 18 ErrTruncatedFrame) of a size check that
+ * ends the capture on the way to the transport check (IPv6 UDP / UDPLite: the
+ * error pcap records in its place), else 0; or LNX_EINVAL.  802.3 length
+ * frames, VLAN-tagged frames and other EtherTypes have no checksum stage in
+ * pcap (status 0 unless their Ethernet size check fails). */
+#define LNX_PCAP_IP_HDR_BAD 1u /* ErrBadCRC in the IPv4 frame's Errors */
+#define LNX_PCAP_PROTO_BAD 2u  /* ipProtoErr == ErrBadCRC (the transport frame's Errors) */
+int lnx_pcap_checksums(const uint8_t* frame, size_t len);
+
 /* The transmit checksum step of ONE frame on the host, in place: the per-frame
  * semantics of lnx_tx_checksum_batch (encapsulate4 / encapsulate6 / the ICMP
  * clients, internet/stack-ip4.go:202-228, internet/stack-ip6.go:167-181).
@@ -288,6 +306,13 @@ int lnx_ingress_verify_batch_filtered(const uint8_t* d_bytes, const uint64_t* d_
  * runs it for its batches. */
 int lnx_rx_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint32_t flags,
                         const lnx_rx_filter* filter, uint8_t* d_fcs_ok, uint8_t* d_verdict, void* stream);
+
+/* pcap's checksum re-verification over a batch: d_status[i] =
+ * lnx_pcap_checksums(d_bytes[d_off[i] : d_off[i+1]]) for every Ethernet frame
+ * (FCS stripped; an end offset below its start is an empty frame).  One wave
+ * per frame; every offset order is allowed. */
+int lnx_pcap_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_status,
+                          void* stream);
 
 /* Host-memory convenience: copies h_bytes/h_off to the device, runs
  * lnx_crc32_batch, copies the CRCs back, synchronously.  Used to measure the

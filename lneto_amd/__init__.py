@@ -132,6 +132,8 @@ _sig = {
     "lnx_rx_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(RxFilter),
                                             _vp, _vp, _vp]),
     "lnx_ingress_verdict": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.POINTER(RxFilter)]),
+    "lnx_pcap_checksums": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "lnx_pcap_verify_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "lnx_tx_checksum": (ctypes.c_int, [_vp, ctypes.c_size_t]),
     "lnx_fcs_append": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "lnx_rx_ring_set_host_threshold": (ctypes.c_int, [_vp, ctypes.c_uint32]),
@@ -482,6 +484,34 @@ def rx_verify_batch(d_bytes, d_off, flags: int = 0, filter: RxFilter | None = No
                                            ctypes.byref(filter) if filter is not None else None, ok.data_ptr(),
                                            verdict.data_ptr(), s), what)
     return ok, verdict
+
+
+PCAP_IP_HDR_BAD, PCAP_PROTO_BAD = 1, 2  # LNX_PCAP_IP_HDR_BAD, LNX_PCAP_PROTO_BAD
+
+
+def pcap_checksums(frame: bytes) -> int:
+    """pcap's checksum findings for ONE Ethernet frame on the host
+    (lnx_pcap_checksums, internet/pcap/capture.go:67-277): PCAP_IP_HDR_BAD |
+    PCAP_PROTO_BAD | code << 2."""
+    buf = bytes(frame)
+    rc = lib.lnx_pcap_checksums(buf, len(buf))
+    if rc < 0:
+        _check(rc, "lnx_pcap_checksums")
+    return rc
+
+
+def pcap_verify_batch(d_bytes, d_off, out=None, stream=None):
+    """pcap's checksum findings per Ethernet frame d_bytes[d_off[i]:d_off[i+1]]
+    (lnx_pcap_verify_batch): a uint8 status tensor, as pcap_checksums."""
+    import torch
+    what = "lnx_pcap_verify_batch"
+    b = _Batch(what, [("d_bytes", d_bytes, "u8"), ("d_off", d_off, "i64")], stream)
+    n = d_off.numel() - 1
+    out = _out(what, out, n, torch.uint8, "u8", b.device)
+    if n > 0:
+        with b as s:
+            _check(lib.lnx_pcap_verify_batch(d_bytes.data_ptr(), d_off.data_ptr(), n, out.data_ptr(), s), what)
+    return out
 
 
 def sum16_batch(d_bytes, d_off, d_len, d_seed=None, out=None, stream=None):

@@ -38,6 +38,8 @@ hipError_t launch_rx_verify(const uint8_t* bytes, const uint64_t* off, uint64_t 
                             uint8_t* ok, uint8_t* verdict, const uint32_t* seg_len, const RxFilter* filter,
                             const uint32_t* image, int num_cus, hipStream_t stream, bool host = false,
                             const uint32_t* gate = nullptr, uint32_t epoch = 0);
+hipError_t launch_pcap_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint8_t* status, int num_cus,
+                              hipStream_t stream);
 hipError_t launch_ingress_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint32_t flags,
                                  uint8_t* verdict, int num_cus, hipStream_t stream, const uint32_t* seg_len,
                                  uint32_t trim, const RxFilter* filter, uint32_t* gate = nullptr, uint32_t epoch = 0,
@@ -693,6 +695,18 @@ int lnx_rx_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t 
                                         !(flags & LNX_RX_NO_FCS), d_fcs_ok, d_verdict, nullptr, &filt, c->d_rx,
                                         c->num_cus, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "rx_verify_kernel launch");
+  return LNX_OK;
+}
+
+int lnx_pcap_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_status,
+                          void* stream) {
+  if (n == 0) return LNX_OK;
+  if (!d_bytes || !d_off || !d_status) return LNX_EINVAL;
+  DeviceCtx* c = nullptr;
+  int st = get_ctx(&c);
+  if (st != LNX_OK) return st;
+  const hipError_t e = launch_pcap_verify(d_bytes, d_off, n, d_status, c->num_cus, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "pcap_verify_kernel launch");
   return LNX_OK;
 }
 

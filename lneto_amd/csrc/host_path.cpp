@@ -9,7 +9,8 @@
 // below the measured crossover here and never launch for them.  These are the
 // product's own restatements of the reference (the oracle in oracle/ is the
 // checker of both paths), and the same functions are exported per frame:
-// lnx_ingress_verdict, lnx_tx_checksum, lnx_fcs_append (include/lneto_amd.h).
+// lnx_ingress_verdict, lnx_pcap_checksums, lnx_tx_checksum, lnx_fcs_append
+// (include/lneto_amd.h).
 #include <cstdint>
 #include <cstring>
 #include "../../include/lneto_amd.h"
@@ -124,6 +125,70 @@ uint8_t ipv6_verdict(const uint8_t* ip, size_t n, uint32_t flags, const RxFilter
   return 0;
 }
 
+// pcap's CaptureIPv4 checksum findings (internet/pcap/capture.go:203-277):
+// status bits as lnx_pcap_verify_batch
+uint8_t pcap_ipv4(const uint8_t* ip, size_t n) {
+  if (n < 20) return kErrTruncatedFrame << 2;  // ipv4.NewFrame
+  const uint32_t tl = be16(ip + 2), ihl = ip[0] & 15u;  // ValidateSize (ipv4/frame.go:214-227), :212-215
+  if (tl < 20) return kErrInvalidLengthField << 2;
+  if (tl > n) return kErrTruncatedFrame << 2;
+  if (ihl < 5 || ihl * 4 > tl) return kErrInvalidLengthField << 2;
+  uint8_t st = 0;
+  {
+    Crc791 h;  // a bad header sum is recorded and the capture goes on (:229-231)
+    h.write_even(ip, 20);
+    if (lnx_sum16(h.sum) != 0) st |= LNX_PCAP_IP_HDR_BAD;
+  }
+  const uint32_t hl = ihl * 4, proto = ip[9], pn = tl - hl;
+  const uint8_t* pay = ip + hl;
+  if (proto == 6 && pn >= 20) {  // tcp.NewFrame accepts it; ValidateSize ends the capture (:241-251)
+    const uint32_t doff = (uint32_t)(pay[12] >> 4) * 4;
+    if (doff < 20) return st | kErrInvalidLengthField << 2;
+    if (doff > pn) return st | kErrTruncatedFrame << 2;
+    Crc791 c;
+    c.write_even(ip + 12, 8);
+    c.add16(pn);
+    c.add16(proto);
+    if (c.payload_sum16(pay, pn) != 0) st |= LNX_PCAP_PROTO_BAD;
+  } else if (proto == 17 && pn >= 8) {  // udp.NewFrame accepts it (:252-266)
+    const uint32_t ul = be16(pay + 4);
+    if (ul < 8) return st | kErrInvalidLengthField << 2;
+    if (ul > pn) return st | kErrTruncatedFrame << 2;
+    if (be16(pay + 6) != 0) {  // a zero UDP checksum is not checked (:259)
+      Crc791 c;
+      c.write_even(ip + 12, 8);
+      c.add16(ul);
+      c.add16(proto);
+      if (c.payload_sum16(pay, ul) != 0) st |= LNX_PCAP_PROTO_BAD;
+    }
+  } else if (proto == 1 && pn >= 8) {  // icmpv4.NewFrame; summed with no pseudo-header (:267-273)
+    if (Crc791{}.payload_sum16(pay, pn) != 0) st |= LNX_PCAP_PROTO_BAD;
+  }
+  return st;
+}
+
+// pcap's CaptureIPv6 checksum findings (internet/pcap/capture.go:159-201)
+uint8_t pcap_ipv6(const uint8_t* ip, size_t n) {
+  if (n < 40) return kErrTruncatedFrame << 2;  // ipv6.NewFrame
+  const uint32_t pl = be16(ip + 4), proto = ip[6];
+  if (pl + 40 > n) return kErrInvalidLengthField << 2;  // ValidateSize
+  Crc791 c;  // CRCWritePseudo (ipv6/frame.go:104-108)
+  c.write_even(ip + 8, 32);
+  c.add32(pl);
+  c.add32(proto);
+  const uint8_t* pay = ip + 40;
+  if (proto == 6) {
+    if (c.payload_sum16(pay, pl) != 0) return LNX_PCAP_PROTO_BAD;
+  } else if (proto == 17 || proto == 136) {  // UDP and UDPLite (:184-198)
+    if (pl < 8) return kErrTruncatedFrame << 2;
+    const uint32_t ul = be16(pay + 4);
+    if (ul < 8) return kErrInvalidLengthField << 2;
+    if (ul > pl) return kErrTruncatedFrame << 2;
+    if (c.payload_sum16(pay, ul) != 0) return LNX_PCAP_PROTO_BAD;  // over the UDP length
+  }
+  return 0;
+}
+
 }  // namespace
 
 // The receive path's checksum-stage verdict of one Ethernet frame without its
@@ -146,6 +211,18 @@ uint8_t host_verdict(const uint8_t* fr, size_t L, uint32_t flags, const RxFilter
   if (!et_handler) return kErrPacketDrop;
   if (et == 0x0800) return ipv4_verdict(fr + 14, L - 14, flags, f);
   if (et == 0x86DD) return ipv6_verdict(fr + 14, L - 14, flags, f);
+  return 0;
+}
+
+// pcap's CaptureEthernet checksum findings (internet/pcap/capture.go:67-110):
+// the same status as pcap_verify_kernel
+uint8_t host_pcap(const uint8_t* fr, size_t L) {
+  if (L < 14) return kErrTruncatedFrame << 2;  // ethernet.NewFrame
+  const uint32_t et = be16(fr + 12);
+  if (et <= 1500 && L < et) return kErrInvalidLengthField << 2;  // ValidateSize
+  if (et == 0x8100 && L < 18) return kErrTruncatedFrame << 2;
+  if (et == 0x0800) return pcap_ipv4(fr + 14, L - 14);  // size and VLAN frames end at :88-97
+  if (et == 0x86DD) return pcap_ipv6(fr + 14, L - 14);
   return 0;
 }
 
@@ -249,6 +326,11 @@ int lnx_ingress_verdict(const uint8_t* frame, size_t len, uint32_t flags, const 
   if (!lnx::rx_filter_of(filter, &f)) return LNX_EINVAL;
   if (len > 0 && !frame) return LNX_EINVAL;
   return lnx::host_verdict(frame, len, flags & (LNX_VERIFY_EVIL_BIT | LNX_VERIFY_ICMP), f);
+}
+
+int lnx_pcap_checksums(const uint8_t* frame, size_t len) {
+  if (len > 0 && !frame) return LNX_EINVAL;
+  return lnx::host_pcap(frame, len);
 }
 
 int lnx_tx_checksum(uint8_t* frame, size_t len) {

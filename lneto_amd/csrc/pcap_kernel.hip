@@ -1,0 +1,169 @@
+// pcap_kernel.hip — pcap's checksum re-verification over a batch, gfx950
+// (the verify callers; the capture tool's variant).
+//
+// For every Ethernet frame, the status lneto's packet-capture breakdown records
+// about its checksums (PacketBreakdown.CaptureEthernet / CaptureIPv4 /
+// CaptureIPv6, internet/pcap/capture.go:67-277), which differs from the
+// receive path's (ingress_kernel.hip):
+//   - a bad IPv4 header sum is recorded and the transport check still runs
+//     (:229-231);
+//   - on IPv4 the TCP / UDP checks run only when tcp / udp.NewFrame accept the
+//     payload, and their size checks end the capture (:241-266); a UDP
+//     checksum of 0 is not checked (:259); ICMPv4 is always summed, with no
+//     pseudo-header (:267-273);
+//   - IPv6 sums TCP over the payload and UDP / UDPLite over the UDP length
+//     (:179-199), the pseudo-header from CRCWritePseudo (ipv6/frame.go:104-108).
+// status = bit 0 IPv4 header sum bad, bit 1 transport sum bad, bits 2-7 the
+// errGeneric code (errors.go:6-28) of a size check that ends the capture on the
+// way to the transport check (IPv6 UDP: the one recorded in its place).
+//
+// Layout: one wave per frame, frames grid-strided.  The wave's 64 lanes hold
+// the frame's first 128 bytes (two byte loads each); every header field is
+// read from them with v_readlane, so the whole decision is scalar.  One pass
+// of 16-byte lane loads over the covering 16-byte blocks then sums the header
+// [14, 34) and the transport bytes (pseudo-header addresses + segment) at once:
+// two (E, O) pairs of v_dot4_u32_u8 sums of the bytes at even / odd frame
+// offsets (every segment starts at an even offset, so its sum of big-endian
+// words is 256 E + O, as in sum16_kernel.hip).  A block holding one of the
+// frame's bytes lies in that byte's page, so the loads never fault.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lnx {
+
+constexpr int kPcapBlock = 256;
+constexpr uint32_t kPcapErrInvalidLengthField = 15, kPcapErrTruncatedFrame = 18;
+
+__device__ __forceinline__ uint32_t pcap_keep_from(int32_t lo) {
+  lo = lo < 0 ? 0 : (lo > 4 ? 4 : lo);
+  return (uint32_t)(0xFFFFFFFFull << (8 * lo));
+}
+// byte mask of the frame offsets [a, b) inside the dword whose byte 0 is at o
+__device__ __forceinline__ uint32_t pcap_range(int32_t o, int32_t a, int32_t b) {
+  return pcap_keep_from(a - o) & ~pcap_keep_from(b - o);
+}
+
+__device__ __forceinline__ uint32_t pcap_fold(uint32_t sum) {  // crc.go:17-21
+  sum = (sum & 0xffffu) + (sum >> 16);
+  return (uint16_t)~(uint16_t)(sum + (sum >> 16));
+}
+
+__global__ void __launch_bounds__(kPcapBlock)
+pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
+                   uint8_t* __restrict__ status) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t stride = (uint64_t)gridDim.x * (kPcapBlock / 64);
+  for (uint64_t f = (uint64_t)blockIdx.x * (kPcapBlock / 64) + wave; f < n; f += stride) {
+    const uint64_t s = off[f], e = off[f + 1];
+    const uint64_t L = e > s ? e - s : 0;  // an end below its start: an empty frame
+    const uint8_t* p = bytes + s;
+    const uint32_t h0 = lane < L ? p[lane] : 0u;
+    const uint32_t h1 = lane + 64 < L ? p[lane + 64] : 0u;
+    auto B = [&](uint32_t k) -> uint32_t {  // frame byte k < 128, k wave-uniform
+      return (uint32_t)__builtin_amdgcn_readlane((int)(k < 64 ? h0 : h1), (int)(k & 63u));
+    };
+    auto BE16 = [&](uint32_t k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
+
+    uint32_t code = 0, seed = 0;
+    bool sum_h = false, sum_t = false;
+    int32_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;  // transport ranges: pseudo-header addresses, segment
+    if (L < 14) {
+      code = kPcapErrTruncatedFrame;                       // ethernet.NewFrame (:74-77)
+    } else {
+      const uint32_t et = BE16(12);
+      if (et <= 1500 && L < et) {
+        code = kPcapErrInvalidLengthField;                 // ValidateSize (ethernet/frame.go:119-127)
+      } else if (et == 0x8100 && L < 18) {
+        code = kPcapErrTruncatedFrame;
+      } else if (et == 0x0800) {                           // CaptureIPv4 (:203-277)
+        const uint64_t il = L - 14;
+        const uint32_t tl = BE16(16), ihl = B(14) & 15u;
+        if (il < 20) code = kPcapErrTruncatedFrame;        // ipv4.NewFrame
+        else if (tl < 20) code = kPcapErrInvalidLengthField;  // ValidateSize, first error kept
+        else if (tl > il) code = kPcapErrTruncatedFrame;
+        else if (ihl < 5 || ihl * 4 > tl) code = kPcapErrInvalidLengthField;
+        else {
+          sum_h = true;                                    // CalculateHeaderCRC: bytes [14, 34)
+          const uint32_t proto = B(23), p0 = 14 + ihl * 4, plen = tl - ihl * 4;
+          if (proto == 6 && plen >= 20) {                  // tcp.NewFrame accepts the payload
+            const uint32_t doff = (B(p0 + 12) >> 4) * 4;   // tcp ValidateSize ends the capture
+            if (doff < 20) code = kPcapErrInvalidLengthField;
+            else if (doff > plen) code = kPcapErrTruncatedFrame;
+            else { sum_t = true; a1 = 26; b1 = 34; a2 = p0; b2 = p0 + plen; seed = plen + 6; }
+          } else if (proto == 17 && plen >= 8) {           // udp.NewFrame accepts the payload
+            const uint32_t ul = BE16(p0 + 4);
+            if (ul < 8) code = kPcapErrInvalidLengthField;
+            else if (ul > plen) code = kPcapErrTruncatedFrame;
+            else if (BE16(p0 + 6) != 0) { sum_t = true; a1 = 26; b1 = 34; a2 = p0; b2 = p0 + ul; seed = ul + 17; }
+          } else if (proto == 1 && plen >= 8) {            // icmpv4.NewFrame; no pseudo-header
+            sum_t = true; a2 = p0; b2 = p0 + plen;
+          }
+        }
+      } else if (et == 0x86DD) {                           // CaptureIPv6 (:159-201)
+        const uint64_t il = L - 14;
+        const uint32_t pl = BE16(18), proto = B(20);
+        if (il < 40) code = kPcapErrTruncatedFrame;        // ipv6.NewFrame
+        else if (pl + 40 > il) code = kPcapErrInvalidLengthField;  // ValidateSize
+        else if (proto == 6) { sum_t = true; a1 = 22; b1 = 54 + pl; seed = pl + 6; }
+        else if (proto == 17 || proto == 136) {
+          if (pl < 8) code = kPcapErrTruncatedFrame;       // udp.NewFrame on the payload
+          else {
+            const uint32_t ul = BE16(58);
+            if (ul < 8) code = kPcapErrInvalidLengthField;
+            else if (ul > pl) code = kPcapErrTruncatedFrame;
+            else { sum_t = true; a1 = 22; b1 = 54 + ul; seed = pl + proto; }
+          }
+        }
+      }
+    }
+
+    uint32_t st = code << 2;
+    if (sum_h || sum_t) {
+      const int32_t lo = sum_h ? 14 : (b1 > a1 ? a1 : a2);
+      const int32_t hi = sum_t ? (b2 > a2 ? b2 : b1) : 34;
+      const uintptr_t P = (uintptr_t)p;
+      const int32_t hA = sum_h ? 14 : 0, hB = sum_h ? 34 : 0;
+      uint32_t hE = 0, hO = 0, tE = 0, tO = 0;
+      // o: the frame offset of a lane's 16-byte block (from the block holding byte lo)
+      for (int32_t o = lo - (int32_t)((P + lo) & 15u) + 16 * (int32_t)lane; o < hi; o += 1024) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p + o);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int32_t oj = o + 4 * j;
+          const uint32_t xh = w[j] & pcap_range(oj, hA, hB);
+          const uint32_t xt = w[j] & (pcap_range(oj, a1, b1) | pcap_range(oj, a2, b2));
+          hE = __builtin_amdgcn_udot4(xh, 0x00010001u, hE, false);
+          hO = __builtin_amdgcn_udot4(xh, 0x01000100u, hO, false);
+          tE = __builtin_amdgcn_udot4(xt, 0x00010001u, tE, false);
+          tO = __builtin_amdgcn_udot4(xt, 0x01000100u, tO, false);
+        }
+      }
+      // byte 0 of every dword sits at an even frame offset iff the frame starts at an even address
+      uint32_t hs = (P & 1) ? (hO << 8) + hE : (hE << 8) + hO;
+      uint32_t ts = (P & 1) ? (tO << 8) + tE : (tE << 8) + tO;
+#pragma unroll
+      for (int sft = 1; sft < 64; sft <<= 1) {
+        hs += (uint32_t)__shfl_xor((int)hs, sft);
+        ts += (uint32_t)__shfl_xor((int)ts, sft);
+      }
+      if (sum_h && pcap_fold(hs) != 0) st |= 1u;
+      if (sum_t && pcap_fold(ts + seed) != 0) st |= 2u;
+    }
+    if (lane == 0) status[f] = (uint8_t)st;
+  }
+}
+
+hipError_t launch_pcap_verify(const uint8_t* bytes, const uint64_t* off, uint64_t n, uint8_t* status, int num_cus,
+                              hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  constexpr uint64_t frames_per_block = kPcapBlock / 64;
+  uint64_t grid = (n + frames_per_block - 1) / frames_per_block;
+  const uint64_t cap = (uint64_t)num_cus * 64;  // 16 waves per SIMD's worth of blocks, then grid-stride
+  if (grid > cap) grid = cap;
+  hipLaunchKernelGGL(pcap_verify_kernel, dim3((unsigned)grid), dim3(kPcapBlock), 0, stream, bytes, off, n, status);
+  return hipGetLastError();
+}
+
+}  // namespace lnx

@@ -341,6 +341,106 @@ def ingress_verdict(frame: bytes, flags: int = 0, filt: StackFilter | None = Non
     return 0
 
 
+# ------------------------------------- pcap's checksum re-verification (a17)
+# PacketBreakdown.CaptureEthernet / CaptureIPv4 / CaptureIPv6
+# (internet/pcap/capture.go:67-277) check the sums with semantics of their own:
+# a bad IPv4 header sum is recorded and the protocol check still runs (:229-231),
+# the TCP / UDP checks on IPv4 run only when tcp / udp.NewFrame accept the
+# payload (:241-266), a UDP checksum of 0 is not checked (:259), ICMPv4 is
+# always summed without pseudo-header (:267-273), IPv6 sums UDP and UDPLite over
+# the UDP length (:184-198).  The validator (pc.vld, no flags) keeps the first
+# error added (validation.go:59-66).
+PCAP_IP_HDR_BAD = 1    # ErrBadCRC appended to the IPv4 frame's Errors (:229-231)
+PCAP_PROTO_BAD = 2     # ipProtoErr == ErrBadCRC (attached to the transport frame, :297-299)
+IPPROTO_UDPLITE = 136  # definitions.go:178
+
+
+def _pcap_ipv4(ip: bytes) -> int:
+    if len(ip) < 20:                                   # ipv4.NewFrame (:208-211)
+        return ERR_TRUNCATED_FRAME << 2
+    tl, ihl = _be16(ip, 2), ip[0] & 0xF
+    errs = []                                          # ipv4 ValidateSize (ipv4/frame.go:214-227), :212-215
+    if tl < 20:
+        errs.append(ERR_INVALID_LENGTH_FIELD)
+    if tl > len(ip):
+        errs.append(ERR_TRUNCATED_FRAME)
+    if ihl < 5 or ihl * 4 > tl:
+        errs.append(ERR_INVALID_LENGTH_FIELD)
+    if errs:
+        return errs[0] << 2
+    st = PCAP_IP_HDR_BAD if ipv4_header_sum16(ip) != 0 else 0
+    proto, payload = ip[9], ip[ihl * 4:tl]
+    if proto == IPPROTO_TCP:
+        if len(payload) >= 20:                         # tcp.NewFrame (tcp/frame.go) accepts it
+            doff = (payload[12] >> 4) * 4              # tcp ValidateSize: the error ends the capture (:243-246)
+            if doff < 20:
+                return st | ERR_INVALID_LENGTH_FIELD << 2
+            if doff > len(payload):
+                return st | ERR_TRUNCATED_FRAME << 2
+            if ipv4_tcp_pseudo(ip).payload_sum16(payload) != 0:
+                st |= PCAP_PROTO_BAD
+    elif proto == IPPROTO_UDP:
+        if len(payload) >= 8:                          # udp.NewFrame accepts it
+            ul = _be16(payload, 4)                     # udp ValidateSize (:255-258)
+            if ul < 8:
+                return st | ERR_INVALID_LENGTH_FIELD << 2
+            if ul > len(payload):
+                return st | ERR_TRUNCATED_FRAME << 2
+            if _be16(payload, 6) != 0 and ipv4_udp_pseudo(ip, ul).payload_sum16(payload[:ul]) != 0:
+                st |= PCAP_PROTO_BAD
+    elif proto == IPPROTO_ICMP:
+        if len(payload) >= 8 and CRC791().payload_sum16(payload) != 0:   # icmpv4.NewFrame, :267-273
+            st |= PCAP_PROTO_BAD
+    return st
+
+
+def _pcap_ipv6(ip6: bytes) -> int:
+    if len(ip6) < 40:                                  # ipv6.NewFrame (:164-167)
+        return ERR_TRUNCATED_FRAME << 2
+    pl = _be16(ip6, 4)
+    if pl + 40 > len(ip6):                             # ValidateSize (:168-171)
+        return ERR_INVALID_LENGTH_FIELD << 2
+    proto, payload = ip6[6], ip6[40:40 + pl]
+    if proto == IPPROTO_TCP:
+        if ipv6_pseudo(ip6).payload_sum16(payload) != 0:
+            return PCAP_PROTO_BAD
+    elif proto in (IPPROTO_UDP, IPPROTO_UDPLITE):
+        # a size error here is ipProtoErr (:185-194); CaptureUDP over the rest of
+        # the packet then fails with the same code or records it on the UDP frame
+        if len(payload) < 8:
+            return ERR_TRUNCATED_FRAME << 2
+        ul = _be16(payload, 4)
+        if ul < 8:
+            return ERR_INVALID_LENGTH_FIELD << 2
+        if ul > len(payload):
+            return ERR_TRUNCATED_FRAME << 2
+        if ipv6_pseudo(ip6).payload_sum16(payload[:ul]) != 0:   # :195-198, the UDP length
+            return PCAP_PROTO_BAD
+    return 0
+
+
+def pcap_checksums(frame: bytes) -> int:
+    """What pcap's PacketBreakdown.CaptureEthernet records about one Ethernet
+    frame's checksums (internet/pcap/capture.go:67-277), as a status byte:
+    bit 0 PCAP_IP_HDR_BAD, bit 1 PCAP_PROTO_BAD, bits 2-7 the errGeneric code of
+    a size error met on the way to (or, for IPv6 UDP / UDPLite, in place of) the
+    transport check, else 0.  Frames that are 802.3 length frames, VLAN-tagged or
+    of another EtherType have no checksum stage in pcap: 0 unless their Ethernet
+    size check fails."""
+    if len(frame) < 14:                                # ethernet.NewFrame (:74-77)
+        return ERR_TRUNCATED_FRAME << 2
+    et = _be16(frame, 12)
+    if et <= 1500 and len(frame) < et:                 # ValidateSize (ethernet/frame.go:119-127), :78-81
+        return ERR_INVALID_LENGTH_FIELD << 2
+    if et == ETHERTYPE_VLAN and len(frame) < 18:
+        return ERR_TRUNCATED_FRAME << 2
+    if et == ETHERTYPE_IPV4:                           # :98-104 (size / VLAN frames returned at :88-97)
+        return _pcap_ipv4(frame[14:])
+    if et == ETHERTYPE_IPV6:
+        return _pcap_ipv6(frame[14:])
+    return 0
+
+
 # ------------------------------------------------- TX checksum generate (a16)
 
 

@@ -318,3 +318,85 @@ def filter_frames(seed: int = 21, count: int = 2400) -> list[bytes]:
             b = b[: int(rng.integers(14, max(15, len(b) - 1)))]
         out.append(bytes(b))
     return out
+
+
+def _udp6_pcap(proto: int, pay: bytes, extra: bytes = b"") -> bytes:
+    """An IPv6 UDP / UDPLite packet whose checksum covers the UDP length only,
+    as pcap sums it (internet/pcap/capture.go:184-198), followed by `extra`
+    bytes inside the IPv6 payload but outside the UDP length."""
+    l4 = bytearray(udp(pay)) + extra
+    hdr = bytearray(struct.pack(">IHBB", 0x60000000, len(l4), proto, 64)) + bytes(range(0x20, 0x30)) + IP6_DST
+    ul = 8 + len(pay)
+    l4[6:8] = struct.pack(">H", O.ipv6_pseudo(bytes(hdr)).payload_sum16(bytes(l4[:ul])))
+    return bytes(hdr) + bytes(l4)
+
+
+def pcap_frames(seed: int = 31, count: int = 2400) -> list[bytes]:
+    """Frames for pcap's checksum re-verification (oracle.pcap_checksums):
+    the receive-path mix (frames()) plus what pcap treats differently — a bad
+    IPv4 header sum in front of a good / bad transport sum, IPv4 UDP with a
+    zero checksum, ICMPv4 of any type (good / flipped), IPv6 UDP and UDPLite
+    summed over the UDP length with bytes after it, TCP data offsets below 5 or
+    past the payload, IPv4 TCP payloads under 20 bytes and UDP under 8."""
+    rng = np.random.default_rng(seed)
+
+    def pay(lo=0, hi=1400):
+        return rng.integers(0, 256, size=int(rng.integers(lo, hi)), dtype=np.uint8).tobytes()
+
+    def flip(f: bytes, lo: int, hi: int | None = None) -> bytes:
+        b = bytearray(f)
+        b[int(rng.integers(lo, len(b) if hi is None else hi))] ^= 1 << int(rng.integers(0, 8))
+        return bytes(b)
+
+    out = []
+    base = frames(seed=seed + 1, count=count // 2)
+    for i in range(count - len(base)):
+        kind = i % 12
+        if kind == 0:    # bad header sum (TTL / ID byte), transport good
+            f = flip(ether(0x0800, ipv4(int(rng.choice([1, 6, 17])), tcp(pay()))), 18, 24)
+        elif kind == 1:  # bad header sum and bad transport sum
+            f = flip(flip(ether(0x0800, ipv4(6, tcp(pay(1)))), 22, 23), 34)
+        elif kind == 2:  # IPv4 UDP with checksum 0: not checked, whatever the payload
+            b = bytearray(flip(ether(0x0800, ipv4(17, udp(pay(1)))), 42))
+            b[40:42] = b"\0\0"
+            f = bytes(b)
+        elif kind == 3:  # ICMPv4 of any type, good or flipped
+            f = ether(0x0800, ipv4(1, icmp(int(rng.integers(0, 256)), pay())))
+            if rng.integers(0, 2):
+                f = flip(f, 34)
+        elif kind == 4:  # ICMPv4 under 8 bytes: icmpv4.NewFrame refuses it, no check
+            f = ether(0x0800, ipv4(1, pay(0, 8), fix_l4=False))
+        elif kind == 5:  # IPv6 UDP / UDPLite over the UDP length, bytes after it
+            f = ether(0x86DD, _udp6_pcap(int(rng.choice([17, 136])), pay(), pay(0, 40)))
+            if rng.integers(0, 2):
+                f = flip(f, 54, 54 + 8 + ((f[58] << 8) | f[59]) - 8)
+        elif kind == 6:  # IPv6 UDPLite / UDP size errors
+            b = bytearray(ether(0x86DD, _udp6_pcap(int(rng.choice([17, 136])), pay(0, 30))))
+            m = int(rng.integers(0, 3))
+            if m == 0:
+                b[58:60] = struct.pack(">H", int(rng.integers(0, 8)))        # ul < 8
+            elif m == 1:
+                b[58:60] = struct.pack(">H", len(b) - 54 + int(rng.integers(1, 100)))  # ul > pl
+            else:
+                b = b[:54 + int(rng.integers(0, 8))]                        # pl < 8
+                b[18:20] = struct.pack(">H", len(b) - 54)
+            f = bytes(b)
+        elif kind == 7:  # TCP data offset < 5 or past the payload (the capture ends)
+            b = bytearray(ether(0x0800, ipv4(6, tcp(pay(0, 40)))))
+            b[46] = (int(rng.integers(0, 5)) if rng.integers(0, 2) else 15) << 4
+            f = flip(bytes(b), 22, 23) if rng.integers(0, 2) else bytes(b)
+        elif kind == 8:  # IPv4 TCP payload under 20 bytes: tcp.NewFrame refuses it, no check
+            f = ether(0x0800, ipv4(6, pay(0, 20), fix_l4=False))
+        elif kind == 9:  # IPv4 UDP length errors behind a bad header sum
+            f = flip(ether(0x0800, ipv4(17, udp(pay(), length=int(rng.choice([0, 7, 4000]))))), 22, 23)
+        elif kind == 10:  # IPv6 TCP, any length from 0 (no NewFrame check there)
+            f = ether(0x86DD, ipv6(6, short_tcp6(rng) if rng.integers(0, 2) else tcp(pay())))
+            if rng.integers(0, 3) == 0 and len(f) > 54:
+                f = flip(f, 54)
+        else:            # IPv6 UDP summed the receive path's way (whole payload): pcap's differs
+            f = ether(0x86DD, ipv6(17, udp(pay())) + pay(1, 20))
+            b = bytearray(f)
+            b[18:20] = struct.pack(">H", len(b) - 54)  # the trailing bytes inside pl
+            f = bytes(b)
+        out.append(f)
+    return base + out
