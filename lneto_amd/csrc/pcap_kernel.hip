@@ -17,10 +17,11 @@
 // errGeneric code (errors.go:6-28) of a size check that ends the capture on the
 // way to the transport check (IPv6 UDP: the one recorded in its place).
 //
-// Layout: one wave per frame, frames grid-strided.  The wave's 64 lanes hold
-// the frame's first 128 bytes (two byte loads each); every header field is
-// read from them with v_readlane, so the whole decision is scalar.  One pass
-// of 16-byte lane loads over the covering 16-byte blocks then sums the header
+// Layout: one wave per frame, frames grid-strided.  The wave loads the frame's
+// first 2 KiB at once (two 16-byte blocks per lane, from the block holding
+// byte 0); every header field is read from those registers with v_readlane,
+// so the whole decision is scalar and costs no second round trip.  The same
+// registers (and, past 2 KiB, further 16-byte loads) then sum the header
 // [14, 34) and the transport bytes (pseudo-header addresses + segment) at once:
 // two (E, O) pairs of v_dot4_u32_u8 sums of the bytes at even / odd frame
 // offsets (every segment starts at an even offset, so its sum of big-endian
@@ -48,6 +49,31 @@ __device__ __forceinline__ uint32_t pcap_fold(uint32_t sum) {  // crc.go:17-21
   return (uint16_t)~(uint16_t)(sum + (sum >> 16));
 }
 
+// a frame's first kPcapWin bytes come in with two 16-byte loads per lane
+// issued before the header is parsed (the window's blocks: lane and lane + 64)
+constexpr int32_t kPcapWin = 2048;
+
+__device__ __forceinline__ uint32_t pcap_dword(const uint4& v, uint32_t d) {  // d wave-uniform
+  return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+// the sums' contributions of one 16-byte block at frame offset o
+__device__ __forceinline__ void pcap_block(const uint4& v, int32_t o, int32_t hA, int32_t hB, int32_t a1, int32_t b1,
+                                           int32_t a2, int32_t b2, uint32_t& hE, uint32_t& hO, uint32_t& tE,
+                                           uint32_t& tO) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int32_t oj = o + 4 * j;
+    const uint32_t xh = w[j] & pcap_range(oj, hA, hB);
+    const uint32_t xt = w[j] & (pcap_range(oj, a1, b1) | pcap_range(oj, a2, b2));
+    hE = __builtin_amdgcn_udot4(xh, 0x00010001u, hE, false);
+    hO = __builtin_amdgcn_udot4(xh, 0x01000100u, hO, false);
+    tE = __builtin_amdgcn_udot4(xt, 0x00010001u, tE, false);
+    tO = __builtin_amdgcn_udot4(xt, 0x01000100u, tO, false);
+  }
+}
+
 __global__ void __launch_bounds__(kPcapBlock)
 pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t n,
                    uint8_t* __restrict__ status) {
@@ -58,10 +84,18 @@ pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     const uint64_t s = off[f], e = off[f + 1];
     const uint64_t L = e > s ? e - s : 0;  // an end below its start: an empty frame
     const uint8_t* p = bytes + s;
-    const uint32_t h0 = lane < L ? p[lane] : 0u;
-    const uint32_t h1 = lane + 64 < L ? p[lane + 64] : 0u;
-    auto B = [&](uint32_t k) -> uint32_t {  // frame byte k < 128, k wave-uniform
-      return (uint32_t)__builtin_amdgcn_readlane((int)(k < 64 ? h0 : h1), (int)(k & 63u));
+    const int32_t q = (int32_t)((uintptr_t)p & 15u);
+    const uint8_t* base = p - q;  // the window: 16-byte blocks from the one holding byte 0
+    // blocks holding frame bytes, up to the window's 128
+    const uint64_t nb64 = L == 0 ? 0 : ((uint64_t)q + L + 15) >> 4;
+    const uint32_t nb = nb64 < 128 ? (uint32_t)nb64 : 128u;
+    uint4 v0{0u, 0u, 0u, 0u}, v1{0u, 0u, 0u, 0u};
+    if (lane < nb) v0 = *reinterpret_cast<const uint4*>(base + 16 * lane);
+    if (lane + 64 < nb) v1 = *reinterpret_cast<const uint4*>(base + 16 * (lane + 64));
+    auto B = [&](uint32_t k) -> uint32_t {  // frame byte k < 128 (block < 9: v0), k wave-uniform
+      const uint32_t a = (uint32_t)q + k;
+      const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)pcap_dword(v0, (a >> 2) & 3u), (int)(a >> 4));
+      return k < L ? (word >> (8 * (a & 3u))) & 0xFFu : 0u;
     };
     auto BE16 = [&](uint32_t k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
 
@@ -120,29 +154,18 @@ pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
 
     uint32_t st = code << 2;
     if (sum_h || sum_t) {
-      const int32_t lo = sum_h ? 14 : (b1 > a1 ? a1 : a2);
       const int32_t hi = sum_t ? (b2 > a2 ? b2 : b1) : 34;
-      const uintptr_t P = (uintptr_t)p;
       const int32_t hA = sum_h ? 14 : 0, hB = sum_h ? 34 : 0;
       uint32_t hE = 0, hO = 0, tE = 0, tO = 0;
-      // o: the frame offset of a lane's 16-byte block (from the block holding byte lo)
-      for (int32_t o = lo - (int32_t)((P + lo) & 15u) + 16 * (int32_t)lane; o < hi; o += 1024) {
-        const uint4 v = *reinterpret_cast<const uint4*>(p + o);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int32_t oj = o + 4 * j;
-          const uint32_t xh = w[j] & pcap_range(oj, hA, hB);
-          const uint32_t xt = w[j] & (pcap_range(oj, a1, b1) | pcap_range(oj, a2, b2));
-          hE = __builtin_amdgcn_udot4(xh, 0x00010001u, hE, false);
-          hO = __builtin_amdgcn_udot4(xh, 0x01000100u, hO, false);
-          tE = __builtin_amdgcn_udot4(xt, 0x00010001u, tE, false);
-          tO = __builtin_amdgcn_udot4(xt, 0x01000100u, tO, false);
-        }
-      }
+      // the window's blocks from registers (ranges outside [0, L) never reach
+      // them: every range ends at or below L), then past the window from memory
+      pcap_block(v0, 16 * (int32_t)lane - q, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
+      pcap_block(v1, 16 * (int32_t)(lane + 64) - q, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
+      for (int32_t o = kPcapWin - q + 16 * (int32_t)lane; o < hi; o += 1024)
+        pcap_block(*reinterpret_cast<const uint4*>(p + o), o, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
       // byte 0 of every dword sits at an even frame offset iff the frame starts at an even address
-      uint32_t hs = (P & 1) ? (hO << 8) + hE : (hE << 8) + hO;
-      uint32_t ts = (P & 1) ? (tO << 8) + tE : (tE << 8) + tO;
+      uint32_t hs = (q & 1) ? (hO << 8) + hE : (hE << 8) + hO;
+      uint32_t ts = (q & 1) ? (tO << 8) + tE : (tE << 8) + tO;
 #pragma unroll
       for (int sft = 1; sft < 64; sft <<= 1) {
         hs += (uint32_t)__shfl_xor((int)hs, sft);
