@@ -80,22 +80,36 @@ pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t stride = (uint64_t)gridDim.x * (kPcapBlock / 64);
-  for (uint64_t f = (uint64_t)blockIdx.x * (kPcapBlock / 64) + wave; f < n; f += stride) {
-    const uint64_t s = off[f], e = off[f + 1];
+  // the window of frame [s, e): 16-byte blocks from the one holding byte 0,
+  // those holding frame bytes up to the window's 128
+  auto window = [&](uint64_t s, uint64_t e, uint4& v0, uint4& v1) {
+    const uint64_t L = e > s ? e - s : 0;
+    const uint8_t* p = bytes + s;
+    const uint32_t q = (uint32_t)((uintptr_t)p & 15u);
+    const uint64_t nb64 = L == 0 ? 0 : ((uint64_t)q + L + 15) >> 4;
+    const uint32_t nb = nb64 < 128 ? (uint32_t)nb64 : 128u;
+    // a buffer descriptor of nb blocks: the range check returns 0 for the
+    // blocks past them, so every lane issues both loads (no branch around
+    // them, and the wait before this frame's use counts the next frame's
+    // loads instead of draining them); an empty frame touches no memory
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p - q), 0, (int)(16 * nb), 0x00020000);
+    const auto r0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, 0, 0);
+    const auto r1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * (lane + 64), 0, 0);
+    v0 = uint4{r0[0], r0[1], r0[2], r0[3]};
+    v1 = uint4{r1[0], r1[1], r1[2], r1[3]};
+  };
+  // the status of frame f = [s, e) from its window v0, v1
+  auto check = [&](uint64_t f, uint64_t s, uint64_t e, const uint4& v0, const uint4& v1) {
     const uint64_t L = e > s ? e - s : 0;  // an end below its start: an empty frame
     const uint8_t* p = bytes + s;
     const int32_t q = (int32_t)((uintptr_t)p & 15u);
-    const uint8_t* base = p - q;  // the window: 16-byte blocks from the one holding byte 0
-    // blocks holding frame bytes, up to the window's 128
-    const uint64_t nb64 = L == 0 ? 0 : ((uint64_t)q + L + 15) >> 4;
-    const uint32_t nb = nb64 < 128 ? (uint32_t)nb64 : 128u;
-    uint4 v0{0u, 0u, 0u, 0u}, v1{0u, 0u, 0u, 0u};
-    if (lane < nb) v0 = *reinterpret_cast<const uint4*>(base + 16 * lane);
-    if (lane + 64 < nb) v1 = *reinterpret_cast<const uint4*>(base + 16 * (lane + 64));
-    auto B = [&](uint32_t k) -> uint32_t {  // frame byte k < 128 (block < 9: v0), k wave-uniform
+    // frame byte k < 128 (block < 9: v0), k wave-uniform.  Every byte the
+    // checks below use lies inside the frame (each is read after the length
+    // check that covers it), so bytes past L need no masking here
+    auto B = [&](uint32_t k) -> uint32_t {
       const uint32_t a = (uint32_t)q + k;
       const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)pcap_dword(v0, (a >> 2) & 3u), (int)(a >> 4));
-      return k < L ? (word >> (8 * (a & 3u))) & 0xFFu : 0u;
+      return (word >> (8 * (a & 3u))) & 0xFFu;
     };
     auto BE16 = [&](uint32_t k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
 
@@ -175,6 +189,35 @@ pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
       if (sum_t && pcap_fold(ts + seed) != 0) st |= 2u;
     }
     if (lane == 0) status[f] = (uint8_t)st;
+  };
+  // two frames in flight per wave: the next one's offsets and window load
+  // while this one is checked; the roles alternate (A, B) so that no register
+  // copy waits for a window early
+  uint64_t f = (uint64_t)blockIdx.x * (kPcapBlock / 64) + wave;
+  if (f >= n) return;
+  uint64_t sA = off[f], eA = off[f + 1], sB = 0, eB = 0;
+  uint4 xa0, xa1, xb0, xb1;
+  window(sA, eA, xa0, xa1);
+  // (the next window's loads are issued unconditionally, an empty one past
+  // the wave's last frame: a load skipped on one path would make the compiler
+  // wait for every load before this frame's first use)
+  for (;;) {
+    uint64_t fn = f + stride;
+    bool more = fn < n;
+    sB = off[more ? fn : f];
+    eB = more ? off[fn + 1] : sB;
+    window(sB, eB, xb0, xb1);
+    check(f, sA, eA, xa0, xa1);
+    if (!more) break;
+    f = fn;
+    fn = f + stride;
+    more = fn < n;
+    sA = off[more ? fn : f];
+    eA = more ? off[fn + 1] : sA;
+    window(sA, eA, xa0, xa1);
+    check(f, sB, eB, xb0, xb1);
+    if (!more) break;
+    f = fn;
   }
 }
 
