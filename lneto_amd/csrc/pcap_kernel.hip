@@ -19,8 +19,10 @@
 //
 // Layout: one wave per frame, frames grid-strided.  The wave loads the frame's
 // first 2 KiB at once (two 16-byte blocks per lane, from the block holding
-// byte 0); every header field is read from those registers with v_readlane,
-// so the whole decision is scalar and costs no second round trip.  The same
+// byte 0); the header's first 128 bytes are realigned across lanes into
+// frame-aligned dwords (ds_bpermute + v_alignbyte) and every header field is
+// a v_readlane of one of them, so the whole decision is scalar and costs no
+// second round trip.  The same
 // registers (and, past 2 KiB, further 16-byte loads) then sum the header
 // [14, 34) and the transport bytes (pseudo-header addresses + segment) at once:
 // two (E, O) pairs of v_dot4_u32_u8 sums of the bytes at even / odd frame
@@ -52,10 +54,6 @@ __device__ __forceinline__ uint32_t pcap_fold(uint32_t sum) {  // crc.go:17-21
 // a frame's first kPcapWin bytes come in with two 16-byte loads per lane
 // issued before the header is parsed (the window's blocks: lane and lane + 64)
 constexpr int32_t kPcapWin = 2048;
-
-__device__ __forceinline__ uint32_t pcap_dword(const uint4& v, uint32_t d) {  // d wave-uniform
-  return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
-}
 
 // the sums' contributions of one 16-byte block at frame offset o
 __device__ __forceinline__ void pcap_block(const uint4& v, int32_t o, int32_t hA, int32_t hB, int32_t a1, int32_t b1,
@@ -103,13 +101,25 @@ pcap_verify_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict
     const uint64_t L = e > s ? e - s : 0;  // an end below its start: an empty frame
     const uint8_t* p = bytes + s;
     const int32_t q = (int32_t)((uintptr_t)p & 15u);
-    // frame byte k < 128 (block < 9: v0), k wave-uniform.  Every byte the
-    // checks below use lies inside the frame (each is read after the length
-    // check that covers it), so bytes past L need no masking here
-    auto B = [&](uint32_t k) -> uint32_t {
-      const uint32_t a = (uint32_t)q + k;
-      const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)pcap_dword(v0, (a >> 2) & 3u), (int)(a >> 4));
-      return (word >> (8 * (a & 3u))) & 0xFFu;
+    // The header as frame-aligned dwords: lane l < 32 holds frame bytes
+    // [4l, 4l + 4), window dwords j + l and j + l + 1 (j = q / 4) joined by
+    // v_alignbyte at q % 4; the window dwords come from their lanes by
+    // ds_bpermute (the four of lane (j + l) / 4 and the first of the next).
+    // Then a header byte is one v_readlane at a wave-uniform lane index.
+    // Every byte the checks below use lies inside the frame (each is read
+    // after the length check that covers it), so bytes past L need no masking
+    const uint32_t dw = ((uint32_t)q >> 2) + lane, src = (dw >> 2) << 2;
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)v0.x);
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)v0.y);
+    const uint32_t c2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)v0.z);
+    const uint32_t c3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)v0.w);
+    const uint32_t n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src + 4, (int)v0.x);
+    const uint32_t sel = dw & 3u;
+    const uint32_t lo = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+    const uint32_t hi = sel == 0 ? c1 : sel == 1 ? c2 : sel == 2 ? c3 : n0;
+    const uint32_t H = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)q & 3u);
+    auto B = [&](uint32_t k) -> uint32_t {  // frame byte k < 128, k wave-uniform
+      return ((uint32_t)__builtin_amdgcn_readlane((int)H, (int)(k >> 2)) >> (8 * (k & 3u))) & 0xFFu;
     };
     auto BE16 = [&](uint32_t k) -> uint32_t { return (B(k) << 8) | B(k + 1); };
 
