@@ -124,7 +124,7 @@ def test_product_library_holds_only_product_kernels():
     others = sorted(re.sub(r"^_ZN3lnx\d+(\w+?kernel).*$", r"\1", k) for k in ks if k not in rows)
     # ingress: filtered / unfiltered verdicts, TX generate; rx_verify: (FCS / none) x (filter / none) x
     # (HBM / host memory); tx_finish: (FCS / none) x (checksum / none) x (HBM / host memory)
-    assert others == (["crc32_search_o_kernel"] + ["crc32_stage_kernel"] * 2 + ["ingress_verify_kernel"] * 3 + ["pcap_verify_kernel"] +
+    assert others == (["crc32_search_o_kernel"] + ["crc32_stage_kernel"] * 2 + ["ingress_verify_kernel"] * 3 + ["pcap_rows_kernel"] +
                       ["ring_segments_kernel"] + ["rx_verify_kernel"] * 8 + ["sum16_lines_kernel"] + ["tx_finish_kernel"] * 8 +
                       ["tx_gate_probe_kernel"]), others
     stage = [k for k in ks if "crc32_stage_kernel" in k]
