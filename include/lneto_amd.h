@@ -309,8 +309,8 @@ int lnx_rx_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t 
 
 /* pcap's checksum re-verification over a batch: d_status[i] =
  * lnx_pcap_checksums(d_bytes[d_off[i] : d_off[i+1]]) for every Ethernet frame
- * (FCS stripped; an end offset below its start is an empty frame).  One wave
- * per frame; every offset order is allowed. */
+ * (FCS stripped; an end offset below its start is an empty frame).  Four
+ * frames per wave (16-lane rows); every offset order is allowed. */
 int lnx_pcap_verify_batch(const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* d_status,
                           void* stream);
 
