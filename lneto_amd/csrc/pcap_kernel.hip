@@ -97,6 +97,8 @@ pcap_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const uint32_t q = (uint32_t)((uintptr_t)p & 15u);
     const uint64_t nb64 = L == 0 ? 0 : ((uint64_t)q + L + 15) >> 4;
     const uint32_t nb = nb64 < (uint64_t)(16 * kPcapSlots) ? (uint32_t)nb64 : 16u * kPcapSlots;
+    const uint32_t nbmax = max(max((uint32_t)__builtin_amdgcn_readlane((int)nb, 0), (uint32_t)__builtin_amdgcn_readlane((int)nb, 16)),
+                               max((uint32_t)__builtin_amdgcn_readlane((int)nb, 32), (uint32_t)__builtin_amdgcn_readlane((int)nb, 48)));
     uint4 w[kPcapSlots];
 #pragma unroll
     for (int k = 0; k < kPcapSlots; ++k) {
@@ -162,8 +164,9 @@ pcap_rows_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__
     const int32_t hi = sum_t ? (b2 > a2 ? b2 : b1) : 34;
     uint32_t hE = 0, hO = 0, tE = 0, tO = 0;
 #pragma unroll
-    for (int k = 0; k < kPcapSlots; ++k)
-      pcap_block(w[k], 16 * (int32_t)(16 * k + rl) - (int32_t)q, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
+    for (int k = 0; k < kPcapSlots; ++k)  // (a slot no row's frame reaches holds zeros: skipped)
+      if (k == 0 || 16u * k < nbmax)
+        pcap_block(w[k], 16 * (int32_t)(16 * k + rl) - (int32_t)q, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
     if (sum_t)  // past the window (frames over ~1.5 KiB)
       for (int32_t o = kPcapRowWin - (int32_t)q + 16 * (int32_t)rl; o < hi; o += 256)
         pcap_block(*reinterpret_cast<const uint4*>(p + o), o, hA, hB, a1, b1, a2, b2, hE, hO, tE, tO);
